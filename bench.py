@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""Benchmark: audio-hours/s of 80-band, p=150 FDLP-spectrogram features on MI355X.
+
+One step = one fdlp_compute over a batch of synthetic 16 kHz utterances already resident in HBM
+(BASELINE.json configs[1]: WSJ si284-like 4 s utterances, 80 bands, p=150, coeff_num=100,
+cochlear filterbank; DESIGN.md "Measurement").  Every rank processes its own batch (utterances
+shard across GPUs with no collective; scaling is weak).  Prints ONE JSON line on rank 0.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config wsj|reverb]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) dense peak, AMD spec
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def speech_like_batch(n_utt, T, seed):
+    """AR(2)-coloured Gaussian noise x 3-5 Hz syllabic envelope, RMS ~2000, int16."""
+    from scipy.signal import lfilter
+    rng = np.random.default_rng(seed)
+    out = np.empty((n_utt, T), dtype=np.int16)
+    t = np.arange(T) / 16000.0
+    for i in range(n_utt):
+        e = rng.standard_normal(T + 400)
+        f0, rad = rng.uniform(400, 1500), rng.uniform(0.90, 0.98)
+        x = lfilter([1.0], [1.0, -2 * rad * np.cos(2 * np.pi * f0 / 16000), rad * rad], e)[400:]
+        x *= 0.55 + 0.45 * np.sin(2 * np.pi * rng.uniform(3, 5) * t + rng.uniform(0, 6.28))
+        x *= 2000.0 / (np.sqrt(np.mean(x * x)) + 1e-12)
+        out[i] = np.clip(np.round(x), -32768, 32767).astype(np.int16)
+    return out
+
+
+def _cpu_worker(args):
+    cfg_name, utts, seed = args
+    os.environ["OMP_NUM_THREADS"] = "1"
+    import random
+    from oracle import fdlp_oracle as O
+    orc = O.FdlpOracle(getattr(O.FdlpConfig, cfg_name)())
+    rng = random.Random(seed)
+    t0 = time.perf_counter()
+    for x in utts:
+        orc.utterance(x, rng)
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(cfg_name, T, workers, per_worker):
+    """The oracle (reference-equivalent fp64 numpy restatement) on a bounded sample."""
+    sig = speech_like_batch(workers * per_worker, T, 4242)
+    jobs = [(cfg_name, [sig[w * per_worker + i] for i in range(per_worker)], 100 + w) for w in range(workers)]
+    ctx = mp.get_context("fork")
+    with ctx.Pool(workers) as pool:
+        times = pool.map(_cpu_worker, jobs)
+    audio_h = workers * per_worker * T / 16000.0 / 3600.0
+    return dict(value=audio_h / max(times), unit="audio-hours/s", cores=workers, kind="port",
+                sample="%d x %.1f s synthetic utterances (%d per process), oracle/fdlp_oracle.py, "
+                       "OMP_NUM_THREADS=1, steady state (plan setup excluded)" %
+                       (workers * per_worker, T / 16000.0, per_worker))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="wsj", choices=["wsj", "reverb"])
+    ap.add_argument("--utts", type=int, default=1024, help="utterances per step per GPU")
+    ap.add_argument("--seconds", type=float, default=4.0, help="utterance length")
+    ap.add_argument("--support-eps", type=float, default=None)
+    ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cpu-per-worker", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    T = int(round(args.seconds * 16000))
+
+    # CPU baseline first (fork before any GPU initialisation in this process)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.config, T, args.cpu_workers, args.cpu_per_worker)
+
+    import torch
+    import torch.distributed as dist
+    from speech_recognition_tools_amd import FdlpPlan, FeatureConfig, PyRandom, DEFAULT_SUPPORT_EPS
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    cfg = getattr(FeatureConfig, args.config)()
+    if args.support_eps is not None:
+        cfg.support_eps = args.support_eps
+    probe = FdlpPlan(cfg, device=-1)
+    F_u, L_u = probe.geometry(T)
+    frames = F_u * args.utts
+    plan = FdlpPlan(cfg, device=local, max_frames=frames)
+    _, lo, hi = probe.fbank()
+    support = (hi - lo).astype(np.int64)
+
+    pcm_host = speech_like_batch(args.utts, T, 1000 + rank)
+    pcm = torch.from_numpy(pcm_host.reshape(-1)).to(dev)
+    lens = [T] * args.utts
+    out = torch.empty((L_u * args.utts, cfg.nfilters), dtype=torch.float32, device=dev)
+    rng = PyRandom(7 + rank)
+    nj = (F_u - 1) * args.utts
+
+    def step():
+        plan.compute(pcm, lens, rng.randbits2(nj), out=out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    plan.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stages, ncalls = plan.stage_times()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    audio_h = world * args.steps * args.utts * T / 16000.0 / 3600.0
+    value = audio_h / elapsed
+    # dominant kernel: the MFMA autocorrelation.  Algorithmic FLOPs = 2 * nlags * (taps in the
+    # band supports) per analysis frame (useful MACs only; DESIGN.md "Roofline").
+    flops_per_launch = 2.0 * plan.nlags * float(support.sum()) * frames
+    ac_ms = stages["autocorr"] / max(ncalls, 1)
+    achieved = flops_per_launch / (ac_ms * 1e-3) / 1e12
+    res = {
+        "metric": "audio-hours/sec FDLP featurized (16 kHz, 80-band)",
+        "value": value,
+        "unit": "audio-hours/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": "wsj_si284_4s_batches" if args.config == "wsj" else "reverb_et_4s_batches",
+                   "utts_per_step_per_gpu": args.utts, "utt_seconds": args.seconds,
+                   "frames_per_step_per_gpu": frames, "nfilters": cfg.nfilters, "order": cfg.order,
+                   "coeff_num": cfg.coeff_num, "fbank": cfg.fbank_type, "support_eps": cfg.support_eps,
+                   "parallelism": "scp-shard x%d (no collective)" % world},
+        "roofline": {"bound": "mfma", "kernel": "autocorr_kernel (v_mfma_f64_16x16x4f64)",
+                     "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                     "avg_launch_ms": ac_ms, "algorithmic_flops_per_launch": flops_per_launch},
+        "stage_ms_per_step": {k: v / max(ncalls, 1) for k, v in stages.items()},
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

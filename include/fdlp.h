@@ -1,0 +1,178 @@
+/*
+ * fdlp.h -- C ABI of libfdlp_hip.so, the MI355X (gfx950) FDLP-spectrogram extractor.
+ *
+ * Drop-in boundary for the reference hot path
+ *   sadhusamik/speech_recognition_tools  src/featgen/computeFDLPSpectrogram.py  getFeats :29-237
+ *   (+ the helpers it imports from src/featgen/features.py).
+ * The reference has no FFI of its own (it is pure Python calling numpy/scipy); the entry points
+ * below are what a ctypes binding of that path needs (INTEGRATION.md shows the binding).
+ * Each function names the reference interface it replaces.
+ *
+ * Conventions: plain C types, caller-owned buffers, no C++ exceptions across the boundary.
+ * Every function returns 0 on success or a negative FDLP_E* code; fdlp_last_error() returns a
+ * thread-local message for the last failure.  "dev" pointers are device (HBM) pointers,
+ * everything else is host memory.  `stream` is a hipStream_t passed as void* (NULL = default).
+ */
+#ifndef FDLP_H
+#define FDLP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FDLP_ABI_VERSION 1
+
+enum {
+  FDLP_OK = 0,
+  FDLP_E_INVALID = -1,   /* bad argument / configuration the reference would reject      */
+  FDLP_E_HIP = -2,       /* HIP runtime failure                                            */
+  FDLP_E_NOMEM = -3,     /* allocation failure                                             */
+  FDLP_E_CAPACITY = -4,  /* batch larger than the plan's max_frames                        */
+  FDLP_E_IO = -5,        /* file read/write failure                                        */
+  FDLP_E_BROADCAST = -6  /* the reference's numpy OLA slicing would raise ValueError here  */
+};
+
+enum { FDLP_FBANK_MEL = 0, FDLP_FBANK_COCHLEAR = 1 };
+enum { FDLP_PCM_I16 = 0, FDLP_PCM_F64 = 1 };
+
+/* Frozen feature configuration.  Mirrors the argparse surface of
+ * computeFDLPSpectrogram.py:240-262 after the parsing getFeats does (:43-118). */
+typedef struct fdlp_config {
+  int32_t nfilters;          /* --nfilters                                   (:245) */
+  int32_t coeff_num;         /* --coeff_num  (M)                             (:246) */
+  int32_t coeff_lp;          /* --coeff_range "lp,hp" -> mask lp<=i<=hp      (:94-103) */
+  int32_t coeff_hp;
+  int32_t order;             /* --order (p)                                  (:248) */
+  int32_t frate;             /* --frate                                      (:250) */
+  int32_t srate;             /* 16000 (getFeats default, :29)                       */
+  int32_t fbank_kind;        /* FDLP_FBANK_MEL | FDLP_FBANK_COCHLEAR          (:49-63) */
+  double fduration;          /* --fduration                                  (:249) */
+  double overlap_fraction;   /* --overlap_fraction (before the 1-x at :104)  (:251) */
+  double warp_fact;          /* mel "mel,wf" / cochlear 6th field                    */
+  double om_w, alp, bet;     /* cochlear "cochlear,om_w,alp,fixed,bet,wf"    (:59-61) */
+  int32_t fixed;
+  int32_t odd_mod_zero;      /* --odd_mod_zero                               (:199-200) */
+  int32_t gamma_enabled;     /* --gamma_weight "scale,shape,pk" (!= "None")  (:107-118) */
+  double gamma_scale, gamma_shape, gamma_pk;
+  const double* lifter;      /* nullable; coeff_num values (--lifter_config first line, :43-46) */
+  int32_t lifter_len;
+  double support_eps;        /* filter taps < eps*peak are skipped in the autocorrelation
+                                (0 = every non-zero tap; DESIGN.md "support")            */
+  int32_t max_frames;        /* workspace capacity: analysis frames per fdlp_compute call  */
+} fdlp_config;
+
+typedef struct fdlp_plan fdlp_plan;
+
+/* Per-call batch of utterances.  Replaces the per-utterance body of getFeats
+ * (computeFDLPSpectrogram.py:159-229): signal -> frames -> DCT -> per-band LPC -> cepstrum ->
+ * envelope -> OLA -> log.  Samples of all utterances are concatenated in one device buffer. */
+typedef struct fdlp_batch {
+  int32_t n_utt;
+  int32_t pcm_kind;              /* FDLP_PCM_I16 (scipy wavfile int16, :139) | FDLP_PCM_F64    */
+  const void* pcm_dev;           /* device: samples                                              */
+  const int64_t* pcm_off;        /* host [n_utt]: first sample of each utterance                 */
+  const int64_t* utt_len;        /* host [n_utt]: T (samples) of each utterance                  */
+  const uint8_t* jitter;         /* host: concatenated randrange(2) draws, F_u-1 per utterance,
+                                    in utterance order (:225); see fdlp_pyrandom_*               */
+  /* optional on-device noise mixing  x = s + alpha*noise[off:off+T]  (features.py:24-31) */
+  const int16_t* noise_dev;      /* nullable device noise samples                                */
+  const int64_t* noise_off;      /* host [n_utt]                                                 */
+  const double* noise_alpha;     /* host [n_utt]                                                 */
+  float* out_dev;                /* device: [sum_u L_u, nfilters] float32, row-major (ark layout) */
+  const int64_t* out_row;        /* host [n_utt]: first output row of each utterance             */
+  double* out_f64_dev;           /* nullable device: same layout, fp64 log features (parity)     */
+  int32_t ark_decimals;          /* >=0: round out_dev like '%.<d>f' text ark (dict2Ark
+                                    features.py:66 uses 3); <0: keep full float32               */
+} fdlp_batch;
+
+/* ---- plan ------------------------------------------------------------------------------- */
+/* Replaces getFeats setup (:43-118): filterbank (features.py:172-219), mask/lifter/gamma
+ * weights, windows, DFT plans; uploads them to `device` and allocates the workspace.
+ * device < 0 creates a host-only plan (geometry, filterbank, weights, OLA tables; no compute). */
+int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out);
+int fdlp_plan_destroy(fdlp_plan* plan);
+const char* fdlp_last_error(void);
+int fdlp_abi_version(void);
+
+/* Frame geometry of one utterance of T samples: F analysis frames (getFrames,
+ * features.py:151) and L output frames (int(ceil(T*frate/srate)), :182). */
+int fdlp_geometry(const fdlp_plan* plan, int64_t T, int32_t* F, int32_t* L);
+/* Plan constants: N (DCT length), nfft, hop, nlags (=order+2), kk (envelope length). */
+int fdlp_plan_info(const fdlp_plan* plan, int32_t* N, int32_t* hop, int32_t* nlags, int32_t* kk,
+                   int32_t* ola_hop);
+/* Host copy of the filterbank [nfilters, nfft/2+1] fp64 (createFbank / createFbankCochlear,
+ * features.py:172-219) and of the per-band tap support [lo, hi). */
+int fdlp_plan_fbank(const fdlp_plan* plan, double* fbank_out, int32_t* lo, int32_t* hi);
+/* Host copy of the folded modulation weights w[coeff_num] (:94-118, :194-200). */
+int fdlp_plan_weights(const fdlp_plan* plan, double* w_out);
+
+/* OLA table of one utterance (computeFDLPSpectrogram.py:207-225): per frame (dst, src, cnt).
+ * Returns FDLP_E_BROADCAST where the reference's numpy slicing raises. */
+int fdlp_ola_table(const fdlp_plan* plan, int64_t T, const uint8_t* jitter, int32_t* dst,
+                   int32_t* src, int32_t* cnt);
+
+/* ---- compute ---------------------------------------------------------------------------- */
+/* Whole pipeline for a batch (getFeats :159-229).  Enqueued on `stream`; host arrays are
+ * consumed before return. */
+int fdlp_compute(fdlp_plan* plan, const fdlp_batch* batch, void* stream);
+/* Reads back the intermediates of the most recent fdlp_compute (parity/debug; synchronous):
+ * any pointer may be NULL.  Layouts: dct [F,N]; r [F,B,nlags]; a [F,B,order+1]; gg [F,B];
+ * cep [F,B,coeff_num]; env [F,B,kk]. */
+int fdlp_debug_fetch(fdlp_plan* plan, int32_t n_frames, double* dct, double* r, double* a,
+                     double* gg, double* cep, double* env);
+
+/* Per-stage device time (HIP events on the compute stream) of every fdlp_compute since profiling
+ * was (re)enabled.  Stages: 0 frames+column DFT, 1 row DFT+DCT, 2 autocorrelation, 3 Levinson,
+ * 4 cepstrum, 5 envelope, 6 OLA+log.  fdlp_stage_times synchronises on the recorded events. */
+#define FDLP_NUM_STAGES 7
+int fdlp_set_profiling(fdlp_plan* plan, int32_t enable);
+int fdlp_stage_times(fdlp_plan* plan, double* ms_sum /* [FDLP_NUM_STAGES] */, int32_t* n_calls);
+
+/* ---- stage entry points (the features.py helpers, batched on the device) --------------- */
+/* scipy.fftpack.dct(x)/sqrt(2N) of n_rows windowed frames [n_rows, N] (computeFDLPSpectrogram
+ * .py:178).  N is the plan's frame length. */
+int fdlp_dct_rows(fdlp_plan* plan, const double* x_dev, int32_t n_rows, double* y_dev,
+                  void* stream);
+/* computeLpcFast (features.py:222-230) for n_items dense band signals [n_items, N]:
+ * a [n_items, order+1] (a0=1), gg [n_items], and the lags r [n_items, order+2]. */
+int fdlp_lpc_rows(fdlp_plan* plan, const double* band_dev, int32_t n_items, double* r_dev,
+                  double* a_dev, double* gg_dev, void* stream);
+/* computeModSpecFromLpc (features.py:233-246): cep [n_items, lim] from a [n_items, p+1], gg. */
+int fdlp_cepstrum_rows(fdlp_plan* plan, const double* a_dev, const double* gg_dev,
+                       int32_t n_items, int32_t p, int32_t lim, double* cep_dev, void* stream);
+
+/* ---- host-side RNG replicas (no device work) --------------------------------------------- */
+/* CPython `random` (MT19937, init_by_array seeding, randrange(2) = getrandbits(2) with
+ * rejection) -- the jitter source of computeFDLPSpectrogram.py:21,225. */
+typedef struct fdlp_pyrandom fdlp_pyrandom;
+int fdlp_pyrandom_create(const uint32_t* key, int32_t key_len, fdlp_pyrandom** out);
+int fdlp_pyrandom_randbits2(fdlp_pyrandom* rng, int64_t n, uint8_t* out);
+int fdlp_pyrandom_destroy(fdlp_pyrandom* rng);
+/* numpy legacy RandomState: seed(int) = init_genrand; rand() = 53-bit double
+ * (features.py:25 noise offset). */
+typedef struct fdlp_nprandom fdlp_nprandom;
+int fdlp_nprandom_create(uint32_t seed, fdlp_nprandom** out);
+int fdlp_nprandom_rand(fdlp_nprandom* rng, int64_t n, double* out);
+int fdlp_nprandom_destroy(fdlp_nprandom* rng);
+/* (offset, alpha) of add_noise_to_wav (features.py:24-31) given the uniform draw u:
+ * energies from int16-wrapped squares exactly like the reference. */
+int fdlp_noise_params(const int16_t* sig, int64_t T, const int16_t* noise, int64_t noise_len,
+                      double snr, double u, int64_t* off, double* alpha);
+
+/* ---- native I/O (replaces scipy.io.wavfile.read :139 and dict2Ark + copy-feats :231) ---- */
+/* Parse a RIFF/WAVE PCM16 mono buffer.  *samples points into `buf`. */
+int fdlp_wav_parse(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* channels,
+                   const int16_t** samples, int64_t* n_samples);
+typedef struct fdlp_ark_writer fdlp_ark_writer;
+/* Kaldi binary ark + scp ("<utt> <abs ark path>:<offset>") like `copy-feats ark,t:- ark,scp:`. */
+int fdlp_ark_open(const char* ark_path, const char* scp_path, fdlp_ark_writer** out);
+int fdlp_ark_write(fdlp_ark_writer* w, const char* utt, const float* mat, int32_t rows,
+                   int32_t cols);
+int fdlp_ark_close(fdlp_ark_writer* w);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FDLP_H */

@@ -1,0 +1,128 @@
+"""ctypes binding of libfdlp_hip.so (include/fdlp.h).
+
+torch is imported first on purpose: torch-ROCm ships its own libamdhip64.so.7 and the
+dynamic linker then resolves this library's libamdhip64.so.7 dependency to that same copy,
+so the process has ONE HIP runtime shared by torch tensors/streams and our kernels.
+
+There is no fallback: if the library is missing the import raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FDLP_LIB", os.path.join(_PKG, "lib", "libfdlp_hip.so"))
+
+FDLP_OK = 0
+FDLP_E_INVALID = -1
+FDLP_E_HIP = -2
+FDLP_E_NOMEM = -3
+FDLP_E_CAPACITY = -4
+FDLP_E_IO = -5
+FDLP_E_BROADCAST = -6
+FDLP_FBANK_MEL = 0
+FDLP_FBANK_COCHLEAR = 1
+FDLP_PCM_I16 = 0
+FDLP_PCM_F64 = 1
+FDLP_NUM_STAGES = 7
+STAGE_NAMES = ("frames_dft1", "dft2_dct", "autocorr", "levinson", "cepstrum", "envelope", "ola_log")
+
+c_i32, c_i64, c_dbl, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
+P_i32 = ctypes.POINTER(c_i32)
+P_i64 = ctypes.POINTER(c_i64)
+P_dbl = ctypes.POINTER(c_dbl)
+P_u8 = ctypes.POINTER(ctypes.c_uint8)
+P_u32 = ctypes.POINTER(ctypes.c_uint32)
+P_i16 = ctypes.POINTER(ctypes.c_int16)
+
+
+class FdlpConfigC(ctypes.Structure):
+    _fields_ = [
+        ("nfilters", c_i32), ("coeff_num", c_i32), ("coeff_lp", c_i32), ("coeff_hp", c_i32),
+        ("order", c_i32), ("frate", c_i32), ("srate", c_i32), ("fbank_kind", c_i32),
+        ("fduration", c_dbl), ("overlap_fraction", c_dbl), ("warp_fact", c_dbl),
+        ("om_w", c_dbl), ("alp", c_dbl), ("bet", c_dbl), ("fixed", c_i32),
+        ("odd_mod_zero", c_i32), ("gamma_enabled", c_i32),
+        ("gamma_scale", c_dbl), ("gamma_shape", c_dbl), ("gamma_pk", c_dbl),
+        ("lifter", P_dbl), ("lifter_len", c_i32), ("support_eps", c_dbl), ("max_frames", c_i32),
+    ]
+
+
+class FdlpBatchC(ctypes.Structure):
+    _fields_ = [
+        ("n_utt", c_i32), ("pcm_kind", c_i32), ("pcm_dev", c_p), ("pcm_off", P_i64),
+        ("utt_len", P_i64), ("jitter", P_u8), ("noise_dev", c_p), ("noise_off", P_i64),
+        ("noise_alpha", P_dbl), ("out_dev", c_p), ("out_row", P_i64), ("out_f64_dev", c_p),
+        ("ark_decimals", c_i32),
+    ]
+
+
+# name -> (restype, argtypes); every function declared in include/fdlp.h
+SIGNATURES = {
+    "fdlp_plan_create": (c_i32, [ctypes.POINTER(FdlpConfigC), c_i32, ctypes.POINTER(c_p)]),
+    "fdlp_plan_destroy": (c_i32, [c_p]),
+    "fdlp_last_error": (ctypes.c_char_p, []),
+    "fdlp_abi_version": (c_i32, []),
+    "fdlp_geometry": (c_i32, [c_p, c_i64, P_i32, P_i32]),
+    "fdlp_plan_info": (c_i32, [c_p, P_i32, P_i32, P_i32, P_i32, P_i32]),
+    "fdlp_plan_fbank": (c_i32, [c_p, P_dbl, P_i32, P_i32]),
+    "fdlp_plan_weights": (c_i32, [c_p, P_dbl]),
+    "fdlp_ola_table": (c_i32, [c_p, c_i64, P_u8, P_i32, P_i32, P_i32]),
+    "fdlp_compute": (c_i32, [c_p, ctypes.POINTER(FdlpBatchC), c_p]),
+    "fdlp_debug_fetch": (c_i32, [c_p, c_i32, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl]),
+    "fdlp_set_profiling": (c_i32, [c_p, c_i32]),
+    "fdlp_stage_times": (c_i32, [c_p, P_dbl, P_i32]),
+    "fdlp_dct_rows": (c_i32, [c_p, c_p, c_i32, c_p, c_p]),
+    "fdlp_lpc_rows": (c_i32, [c_p, c_p, c_i32, c_p, c_p, c_p, c_p]),
+    "fdlp_cepstrum_rows": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_i32, c_p, c_p]),
+    "fdlp_pyrandom_create": (c_i32, [P_u32, c_i32, ctypes.POINTER(c_p)]),
+    "fdlp_pyrandom_randbits2": (c_i32, [c_p, c_i64, P_u8]),
+    "fdlp_pyrandom_destroy": (c_i32, [c_p]),
+    "fdlp_nprandom_create": (c_i32, [ctypes.c_uint32, ctypes.POINTER(c_p)]),
+    "fdlp_nprandom_rand": (c_i32, [c_p, c_i64, P_dbl]),
+    "fdlp_nprandom_destroy": (c_i32, [c_p]),
+    "fdlp_noise_params": (c_i32, [P_i16, c_i64, P_i16, c_i64, c_dbl, c_dbl, P_i64, P_dbl]),
+    "fdlp_wav_parse": (c_i32, [P_u8, c_i64, P_i32, P_i32, ctypes.POINTER(P_i16), P_i64]),
+    "fdlp_ark_open": (c_i32, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(c_p)]),
+    "fdlp_ark_write": (c_i32, [c_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), c_i32, c_i32]),
+    "fdlp_ark_close": (c_i32, [c_p]),
+}
+
+
+class FdlpError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (fdlp code %d)" % (msg, code))
+        self.code = code
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libfdlp_hip.so not built (%s); run __graft_entry__.build() or "
+                          "python -m speech_recognition_tools_amd._build" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.fdlp_abi_version() != 1:
+        raise ImportError("libfdlp_hip.so ABI mismatch")
+    return lib
+
+
+lib = _load()
+
+
+def check(rc):
+    if rc != FDLP_OK:
+        msg = lib.fdlp_last_error()
+        msg = msg.decode("utf-8", "replace") if msg else "unknown error"
+        if rc == FDLP_E_BROADCAST:
+            raise ValueError(msg)
+        raise FdlpError(rc, msg)
+    return rc
+
+
+def ptr(arr, ctype):
+    """numpy array -> ctypes pointer (arr must stay alive)."""
+    return arr.ctypes.data_as(ctypes.POINTER(ctype))

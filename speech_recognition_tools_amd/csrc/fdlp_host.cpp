@@ -1,0 +1,260 @@
+// fdlp_host.cpp -- host-side pieces of libfdlp_hip.so that need no device:
+//   * CPython `random` replica (MT19937 + init_by_array + randrange(2))  -> OLA hop jitter
+//     (computeFDLPSpectrogram.py:21,225)
+//   * numpy legacy RandomState replica (init_genrand + 53-bit rand())      -> noise offset
+//     (features.py:25)
+//   * add_noise_to_wav energies with int16-wrapped squares                  (features.py:24-31)
+//   * RIFF/WAVE PCM16 parser                          (replaces scipy.io.wavfile.read, :133,:139)
+//   * Kaldi binary ark/scp writer               (replaces dict2Ark + copy-feats, features.py:63-69)
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <climits>
+#include <new>
+#include <string>
+
+#include "../../include/fdlp.h"
+#include "fdlp_error.h"
+
+namespace {
+
+struct MT19937 {
+  uint32_t mt[624];
+  int mti = 625;
+  void init_genrand(uint32_t s) {
+    mt[0] = s;
+    for (int i = 1; i < 624; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+    mti = 624;
+  }
+  void init_by_array(const uint32_t* key, int len) {
+    init_genrand(19650218u);
+    int i = 1, j = 0;
+    for (int k = (624 > len ? 624 : len); k; --k) {
+      mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+      ++i;
+      ++j;
+      if (i >= 624) { mt[0] = mt[623]; i = 1; }
+      if (j >= len) j = 0;
+    }
+    for (int k = 623; k; --k) {
+      mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+      ++i;
+      if (i >= 624) { mt[0] = mt[623]; i = 1; }
+    }
+    mt[0] = 0x80000000u;
+    mti = 624;
+  }
+  uint32_t next() {
+    static const uint32_t mag01[2] = {0u, 0x9908b0dfu};
+    if (mti >= 624) {
+      int kk;
+      for (kk = 0; kk < 624 - 397; ++kk) {
+        uint32_t y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+        mt[kk] = mt[kk + 397] ^ (y >> 1) ^ mag01[y & 1u];
+      }
+      for (; kk < 623; ++kk) {
+        uint32_t y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+        mt[kk] = mt[kk + (397 - 624)] ^ (y >> 1) ^ mag01[y & 1u];
+      }
+      uint32_t y = (mt[623] & 0x80000000u) | (mt[0] & 0x7fffffffu);
+      mt[623] = mt[396] ^ (y >> 1) ^ mag01[y & 1u];
+      mti = 0;
+    }
+    uint32_t y = mt[mti++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+  }
+};
+
+}  // namespace
+
+struct fdlp_pyrandom { MT19937 mt; };
+struct fdlp_nprandom { MT19937 mt; };
+
+extern "C" {
+
+int fdlp_pyrandom_create(const uint32_t* key, int32_t key_len, fdlp_pyrandom** out) {
+  if (!out || key_len < 0 || (key_len > 0 && !key)) return fdlp::fail(FDLP_E_INVALID, "fdlp_pyrandom_create: bad args");
+  auto* r = new (std::nothrow) fdlp_pyrandom;
+  if (!r) return fdlp::fail(FDLP_E_NOMEM, "fdlp_pyrandom_create: out of memory");
+  // CPython random.seed(int): key = 32-bit words of |seed|, at least one word ([0] for 0)
+  const uint32_t zero = 0;
+  if (key_len == 0) r->mt.init_by_array(&zero, 1);
+  else r->mt.init_by_array(key, key_len);
+  *out = r;
+  return FDLP_OK;
+}
+
+int fdlp_pyrandom_randbits2(fdlp_pyrandom* rng, int64_t n, uint8_t* out) {
+  if (!rng || n < 0 || (n > 0 && !out)) return fdlp::fail(FDLP_E_INVALID, "fdlp_pyrandom_randbits2: bad args");
+  // randrange(2) -> _randbelow_with_getrandbits(2): k = 2, r = getrandbits(2) until r < 2
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t r;
+    do { r = rng->mt.next() >> 30; } while (r >= 2u);
+    out[i] = (uint8_t)r;
+  }
+  return FDLP_OK;
+}
+
+int fdlp_pyrandom_destroy(fdlp_pyrandom* rng) {
+  delete rng;
+  return FDLP_OK;
+}
+
+int fdlp_nprandom_create(uint32_t seed, fdlp_nprandom** out) {
+  if (!out) return fdlp::fail(FDLP_E_INVALID, "fdlp_nprandom_create: bad args");
+  auto* r = new (std::nothrow) fdlp_nprandom;
+  if (!r) return fdlp::fail(FDLP_E_NOMEM, "fdlp_nprandom_create: out of memory");
+  r->mt.init_genrand(seed);  // numpy legacy seeding of an int seed
+  *out = r;
+  return FDLP_OK;
+}
+
+int fdlp_nprandom_rand(fdlp_nprandom* rng, int64_t n, double* out) {
+  if (!rng || n < 0 || (n > 0 && !out)) return fdlp::fail(FDLP_E_INVALID, "fdlp_nprandom_rand: bad args");
+  for (int64_t i = 0; i < n; ++i) {
+    const uint32_t a = rng->mt.next() >> 5, b = rng->mt.next() >> 6;
+    out[i] = (a * 67108864.0 + b) / 9007199254740992.0;
+  }
+  return FDLP_OK;
+}
+
+int fdlp_nprandom_destroy(fdlp_nprandom* rng) {
+  delete rng;
+  return FDLP_OK;
+}
+
+int fdlp_noise_params(const int16_t* sig, int64_t T, const int16_t* noise, int64_t noise_len, double snr,
+                      double u, int64_t* off, double* alpha) {
+  if (!sig || !noise || !off || !alpha || T <= 0) return fdlp::fail(FDLP_E_INVALID, "fdlp_noise_params: bad args");
+  // rand_num = int(floor(rand() * (len(noise) - len(sig))))            (features.py:25)
+  const double span = (double)(noise_len - T);
+  const int64_t o = (int64_t)floor(u * span);
+  if (o < 0 || o + T > noise_len)
+    return fdlp::fail(FDLP_E_INVALID, "noise file shorter than the utterance (reference slices a short noise)");
+  // E = mean(x**2) with int16 squares (wrapping), accumulated exactly  (features.py:27-28)
+  int64_t es = 0, en = 0;
+  for (int64_t t = 0; t < T; ++t) {
+    es += (int16_t)(uint16_t)((uint32_t)(int32_t)sig[t] * (uint32_t)(int32_t)sig[t]);
+    en += (int16_t)(uint16_t)((uint32_t)(int32_t)noise[o + t] * (uint32_t)(int32_t)noise[o + t]);
+  }
+  const double Es = (double)es / (double)T, En = (double)en / (double)T;
+  *alpha = sqrt(Es / (En * pow(10.0, snr / 10.0)));  // (features.py:29)
+  *off = o;
+  return FDLP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// WAV
+// ---------------------------------------------------------------------------------------------
+static uint32_t rd32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
+static uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+
+int fdlp_wav_parse(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* channels, const int16_t** samples,
+                   int64_t* n_samples) {
+  if (!buf || len < 12 || memcmp(buf, "RIFF", 4) || memcmp(buf + 8, "WAVE", 4))
+    return fdlp::fail(FDLP_E_IO, "not a RIFF/WAVE buffer");
+  int64_t pos = 12;
+  int fmt_ok = 0;
+  uint16_t fmt = 0, ch = 0, bits = 0;
+  uint32_t sr = 0;
+  while (pos + 8 <= len) {
+    const uint8_t* h = buf + pos;
+    uint32_t sz = rd32(h + 4);
+    const int64_t body = pos + 8;
+    if (!memcmp(h, "fmt ", 4)) {
+      if (sz < 16 || body + 16 > len) return fdlp::fail(FDLP_E_IO, "truncated fmt chunk");
+      fmt = rd16(buf + body);
+      ch = rd16(buf + body + 2);
+      sr = rd32(buf + body + 4);
+      bits = rd16(buf + body + 14);
+      if (fmt == 0xFFFE && sz >= 40) fmt = rd16(buf + body + 24);  // WAVE_FORMAT_EXTENSIBLE subformat
+      fmt_ok = 1;
+    } else if (!memcmp(h, "data", 4)) {
+      if (!fmt_ok) return fdlp::fail(FDLP_E_IO, "data chunk before fmt chunk");
+      if (fmt != 1 || bits != 16) return fdlp::fail(FDLP_E_IO, "only PCM16 WAV is supported");
+      int64_t avail = len - body;
+      // scipy tolerates an over-long size field (sox pipes write 0xFFFFFFFF): clamp
+      int64_t nbytes = (int64_t)sz > avail ? avail : (int64_t)sz;
+      if (sz == 0 || sz == 0xFFFFFFFFu) nbytes = avail;
+      if (ch == 0) return fdlp::fail(FDLP_E_IO, "zero channels");
+      *srate = (int32_t)sr;
+      *channels = ch;
+      *samples = (const int16_t*)(buf + body);
+      *n_samples = nbytes / 2 / ch;
+      return FDLP_OK;
+    }
+    pos = body + sz + (sz & 1);
+  }
+  return fdlp::fail(FDLP_E_IO, "no data chunk");
+}
+
+// ---------------------------------------------------------------------------------------------
+// Kaldi ark/scp writer: "<utt> \0B" + "FM " + <int32 size=4 rows> + <int32 size=4 cols> + data
+// ---------------------------------------------------------------------------------------------
+struct fdlp_ark_writer {
+  FILE* ark = nullptr;
+  FILE* scp = nullptr;
+  std::string ark_abs;
+};
+
+int fdlp_ark_open(const char* ark_path, const char* scp_path, fdlp_ark_writer** out) {
+  if (!ark_path || !out) return fdlp::fail(FDLP_E_INVALID, "fdlp_ark_open: bad args");
+  auto* w = new (std::nothrow) fdlp_ark_writer;
+  if (!w) return fdlp::fail(FDLP_E_NOMEM, "fdlp_ark_open: out of memory");
+  w->ark = fopen(ark_path, "wb");
+  if (!w->ark) {
+    delete w;
+    return fdlp::fail(FDLP_E_IO, std::string("cannot open ark ") + ark_path);
+  }
+  if (scp_path) {
+    w->scp = fopen(scp_path, "w");
+    if (!w->scp) {
+      fclose(w->ark);
+      delete w;
+      return fdlp::fail(FDLP_E_IO, std::string("cannot open scp ") + scp_path);
+    }
+  }
+  char* abs = realpath(ark_path, nullptr);
+  w->ark_abs = abs ? abs : ark_path;
+  free(abs);
+  *out = w;
+  return FDLP_OK;
+}
+
+int fdlp_ark_write(fdlp_ark_writer* w, const char* utt, const float* mat, int32_t rows, int32_t cols) {
+  if (!w || !utt || rows < 0 || cols < 0 || (rows * (int64_t)cols > 0 && !mat))
+    return fdlp::fail(FDLP_E_INVALID, "fdlp_ark_write: bad args");
+  if (fprintf(w->ark, "%s ", utt) < 0) return fdlp::fail(FDLP_E_IO, "ark write failed");
+  const long offset = ftell(w->ark);
+  const char hdr[] = {'\0', 'B', 'F', 'M', ' '};
+  const char four = 4;
+  int ok = fwrite(hdr, 1, 5, w->ark) == 5;
+  ok &= fwrite(&four, 1, 1, w->ark) == 1;
+  ok &= fwrite(&rows, 4, 1, w->ark) == 1;
+  ok &= fwrite(&four, 1, 1, w->ark) == 1;
+  ok &= fwrite(&cols, 4, 1, w->ark) == 1;
+  const size_t n = (size_t)rows * (size_t)cols;
+  if (n) ok &= fwrite(mat, sizeof(float), n, w->ark) == n;
+  if (!ok) return fdlp::fail(FDLP_E_IO, "ark write failed");
+  if (w->scp && fprintf(w->scp, "%s %s:%ld\n", utt, w->ark_abs.c_str(), offset) < 0)
+    return fdlp::fail(FDLP_E_IO, "scp write failed");
+  return FDLP_OK;
+}
+
+int fdlp_ark_close(fdlp_ark_writer* w) {
+  if (!w) return FDLP_OK;
+  int rc = FDLP_OK;
+  if (w->ark && fclose(w->ark) != 0) rc = fdlp::fail(FDLP_E_IO, "ark close failed");
+  if (w->scp && fclose(w->scp) != 0) rc = fdlp::fail(FDLP_E_IO, "scp close failed");
+  delete w;
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,85 @@
+// fdlp_internal.h -- structures shared by the host runtime (fdlp_plan.cpp) and the gfx950
+// kernels (fdlp_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fdlp {
+
+constexpr int kMaxRadices = 16;
+
+// A length-n complex DFT factored into radices (Stockham autosort, one LDS-resident pass).
+struct DftPlan {
+  int n;
+  int nrad;
+  int rad[kMaxRadices];
+};
+
+// One analysis frame of the batch (getFrames, features.py:118-154).
+struct FrameDesc {
+  int64_t pcm_off;     // first sample of the utterance in the batch PCM buffer
+  int64_t noise_off;   // noise mixing offset (features.py:25), -1 = none
+  double alpha;        // noise mixing gain (features.py:29)
+  int32_t T;           // utterance length in samples
+  int32_t k;           // frame index inside the utterance
+  int32_t dst, src, cnt;  // OLA slice (computeFDLPSpectrogram.py:207-218)
+  int32_t utt;         // utterance index in the batch
+};
+
+// One utterance of the batch (output side).
+struct UttDesc {
+  int64_t out_row;     // first output row
+  int32_t L;           // output frames
+  int32_t frame0;      // first analysis frame (global index in the batch)
+  int32_t F;           // analysis frames
+  int32_t pad;
+};
+
+// Device-resident constants of a plan.
+struct DevConsts {
+  int B, N, hop, ext, p, nlags, M, Me, kk, env_nfft;
+  const double* fbank;     // [B, N] dense taps (column N of the reference's nfft/2+1 dropped, :190)
+  const int* lo;           // [B] first tap >= eps
+  const int* hi;           // [B] one past the last tap >= eps
+  const double* hamming;   // [N]   np.hamming(N)
+  const double* weights;   // [3, M] mask (:94-103), lifter (:195-196), gamma (:197-198); 1.0 if absent
+  const double* env_cos;   // [env_nfft] cos(2*pi*q/env_nfft)
+  const double* env_win;   // [kk, 2] (hanning(kk)[t], hamming(kk)[t]) interleaved (:205)
+  const double* tw1;       // [N1 * N2] four-step twiddles exp(-2*pi*i*n2*k1/N) (complex)
+  const double* post;      // [N] complex exp(-i*pi*k/(2N)) (Makhoul post-twiddle)
+};
+
+}  // namespace fdlp
+
+// Launch wrappers implemented in fdlp_kernels.hip (host-callable).
+namespace fdlp {
+struct Workspace {
+  double2* z;      // [F, N1, N2] complex (four-step intermediate)
+  double* dct;     // [F, N]
+  double* r;       // [F*B, nlags]
+  double* a;       // [F*B, p+1]
+  double* gg;      // [F*B]
+  double* cep;     // [F*B, M]
+  double* env;     // [F*B, kk]
+};
+
+hipError_t launch_frames_dft1(const DevConsts& c, const DftPlan& d1, int N2, const void* pcm,
+                              int pcm_kind, const int16_t* noise, const FrameDesc* frames,
+                              const double* dense_rows, int nframes, double2* z,
+                              const double2* om1, hipStream_t s);
+hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const double2* z,
+                           int nframes, double* dct, const double2* om2, hipStream_t s);
+hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* dense_rows,
+                           int nframes_or_items, double* r, hipStream_t s);
+hipError_t launch_levinson(const DevConsts& c, const double* r, int items, double* a,
+                           double* gg, hipStream_t s);
+hipError_t launch_cepstrum(int p, int M, const double* a, const double* gg, int items,
+                           double* cep, hipStream_t s);
+hipError_t launch_envelope(const DevConsts& c, int odd_zero, const double* cep, int items,
+                           double* env, hipStream_t s);
+int autocorr_tiles(int nlags);
+constexpr int kDftMaxSub = 512;  // longest LDS-resident sub-DFT of the four-step DCT
+hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc* frames,
+                          const UttDesc* utts, int n_utt, int maxL, float* out,
+                          double* out_f64, int decimals, hipStream_t s);
+}  // namespace fdlp

@@ -1,0 +1,646 @@
+// fdlp_plan.cpp -- plan (setup of getFeats, computeFDLPSpectrogram.py:43-118), batch geometry,
+// OLA tables and the kernel pipeline behind fdlp_compute (getFeats :159-229).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/fdlp.h"
+#include "fdlp_error.h"
+#include "fdlp_internal.h"
+
+namespace fdlp {
+std::string& last_error_slot() {
+  static thread_local std::string s;
+  return s;
+}
+}  // namespace fdlp
+
+using fdlp::fail;
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess)                                                                   \
+      return fail(FDLP_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));          \
+  } while (0)
+
+namespace {
+
+// numpy.linspace(start, stop, num): i*step + start, last element = stop exactly.
+std::vector<double> linspace(double start, double stop, int num) {
+  std::vector<double> y(num);
+  if (num == 1) { y[0] = start; return y; }
+  const double step = (stop - start) / (double)(num - 1);
+  for (int i = 0; i < num; ++i) y[i] = (double)i * step + start;
+  if (num > 1) y[num - 1] = stop;
+  return y;
+}
+
+// numpy.hamming / numpy.hanning: c0 + c1*cos(pi*n/(M-1)), n = 1-M, 3-M, ..., M-1
+std::vector<double> cos_window(int M, double c0, double c1) {
+  std::vector<double> w(std::max(M, 0));
+  if (M == 1) { w[0] = 1.0; return w; }
+  for (int i = 0; i < M; ++i) {
+    const double n = (double)(1 - M + 2 * i);
+    w[i] = c0 + c1 * cos(M_PI * n / (double)(M - 1));
+  }
+  return w;
+}
+
+// createFbankCochlear (features.py:193-219)
+std::vector<double> fbank_cochlear(int nf, int nfft, int srate, double om_w, double alp, int fixed, double bet,
+                                   double wf, int* ncol_out) {
+  auto bark = [wf](double x) { return 6.0 * asinh((x / wf) / 600.0); };
+  const double fmax = (double)srate / 2.0;
+  const std::vector<double> cf = linspace(0.0, bark(fmax), nf);
+  const int ncol = (int)floor((double)nfft / 2.0 + 1.0);
+  std::vector<double> fl = linspace(0.0, fmax, ncol);
+  for (auto& v : fl) v = bark(v);
+  std::vector<double> W((size_t)nf * ncol);
+  for (int i = 0; i < nf; ++i) {
+    const double fc = cf[i];
+    const double a = fixed == 1 ? alp : alp * exp(-0.1 * fc);
+    for (int j = 0; j < ncol; ++j) {
+      const double d = fl[j] - fc;
+      double v;
+      if (d <= -om_w / 2.0) v = pow(10.0, a * (d + om_w / 2.0));
+      else if (d > -om_w / 2.0 && d < om_w / 2.0) v = 1.0;
+      else v = pow(10.0, -bet * (d - om_w / 2.0));
+      W[(size_t)i * ncol + j] = v;
+    }
+  }
+  *ncol_out = ncol;
+  return W;
+}
+
+// createFbank (features.py:172-190)
+std::vector<double> fbank_mel(int nf, int nfft, int srate, double wf, int* ncol_out) {
+  const double mel_max = 2595.0 * log10(1.0 + ((double)srate / wf) / 1400.0);
+  const std::vector<double> mels = linspace(0.0, mel_max, nf + 2);
+  const int ncol = (int)floor((double)nfft / 2.0 + 1.0);
+  std::vector<double> edge(nf + 2);
+  for (int i = 0; i < nf + 2; ++i) {
+    const double hz = wf * (700.0 * (pow(10.0, mels[i] / 2595.0) - 1.0));
+    edge[i] = floor((double)(nfft + 1) * hz / (double)srate);
+  }
+  std::vector<double> W((size_t)nf * ncol, 0.0);
+  for (int m = 1; m <= nf; ++m) {
+    const int l = (int)edge[m - 1], c = (int)edge[m], r = (int)edge[m + 1];
+    for (int k = l; k < c; ++k)
+      if (k >= 0 && k < ncol) W[(size_t)(m - 1) * ncol + k] = ((double)k - edge[m - 1]) / (edge[m] - edge[m - 1]);
+    for (int k = c; k < r; ++k)
+      if (k >= 0 && k < ncol) W[(size_t)(m - 1) * ncol + k] = (edge[m + 1] - (double)k) / (edge[m + 1] - edge[m]);
+  }
+  *ncol_out = ncol;
+  return W;
+}
+
+// radix split of n over the supported radices (4s first, then 2, 3, 5, 7)
+bool factor_radices(int n, fdlp::DftPlan* d) {
+  d->n = n;
+  d->nrad = 0;
+  int m = n;
+  auto push = [d](int r) {
+    if (d->nrad >= fdlp::kMaxRadices) return false;
+    d->rad[d->nrad++] = r;
+    return true;
+  };
+  while (m % 4 == 0) { if (!push(4)) return false; m /= 4; }
+  while (m % 2 == 0) { if (!push(2)) return false; m /= 2; }
+  for (int r : {3, 5, 7})
+    while (m % r == 0) { if (!push(r)) return false; m /= r; }
+  return m == 1;
+}
+
+// split N = N1 * N2 with both sub-DFTs LDS-resident, N1 ~ sqrt(N)
+bool split_four_step(int N, fdlp::DftPlan* d1, fdlp::DftPlan* d2) {
+  int best = -1;
+  for (int n1 = 1; n1 <= N; ++n1) {
+    if (N % n1) continue;
+    const int n2 = N / n1;
+    if (n1 > fdlp::kDftMaxSub || n2 > fdlp::kDftMaxSub) continue;
+    fdlp::DftPlan a, b;
+    if (!factor_radices(n1, &a) || !factor_radices(n2, &b)) continue;
+    if (best < 0 || std::abs(n1 - n2) < std::abs(best - N / best)) best = n1;
+  }
+  if (best < 0) return false;
+  factor_radices(best, d1);
+  factor_radices(N / best, d2);
+  return true;
+}
+
+double gamma_pdf(double x, double a, double loc, double scale) {
+  // scipy.stats.gamma.pdf = exp(xlogy(a-1, y) - y - gammaln(a)) / scale, y = (x-loc)/scale >= 0
+  const double y = (x - loc) / scale;
+  if (!(y >= 0.0)) return 0.0;
+  const double xl = (a - 1.0 == 0.0) ? 0.0 : (a - 1.0) * log(y);
+  return exp(xl - y - lgamma(a)) / scale;
+}
+
+struct StagingHost {
+  std::vector<fdlp::FrameDesc> frames;
+  std::vector<fdlp::UttDesc> utts;
+};
+
+}  // namespace
+
+struct fdlp_plan {
+  fdlp_config cfg{};
+  int device = 0;
+  // geometry (computeFDLPSpectrogram.py / features.py float expressions)
+  int N = 0, nfft = 0, hop = 0, sp_b = 0, sp_f = 0, ext = 0, env_nfft = 0, kk = 0, kkb2 = 0, ola_hop = 0;
+  int B = 0, p = 0, M = 0, nlags = 0, Me = 0, ncol = 0;
+  fdlp::DftPlan d1{}, d2{};
+  std::vector<double> fbank_host;  // [B, ncol]
+  std::vector<int> lo, hi;
+  std::vector<double> weights_host;  // [3, M]
+  // device constants
+  fdlp::DevConsts dc{};
+  double *d_fbank = nullptr, *d_hamming = nullptr, *d_weights = nullptr, *d_env_cos = nullptr,
+         *d_env_win = nullptr, *d_tw1 = nullptr, *d_post = nullptr;
+  double2 *d_om1 = nullptr, *d_om2 = nullptr;
+  int *d_lo = nullptr, *d_hi = nullptr;
+  // workspace
+  int max_frames = 0;
+  fdlp::Workspace ws{};
+  fdlp::FrameDesc* d_frames = nullptr;
+  fdlp::UttDesc* d_utts = nullptr;
+  fdlp::FrameDesc* h_frames = nullptr;  // pinned staging
+  fdlp::UttDesc* h_utts = nullptr;
+  hipEvent_t staging_done = nullptr;
+  bool staging_pending = false;
+  int last_frames = 0;
+  // optional per-stage HIP-event timing (fdlp_set_profiling / fdlp_stage_times)
+  bool profiling = false;
+  std::vector<std::vector<hipEvent_t>> prof_pending;
+  double prof_ms[FDLP_NUM_STAGES] = {0};
+  int prof_calls = 0;
+};
+
+namespace {
+
+int drain_profile(fdlp_plan* p) {
+  for (auto& ev : p->prof_pending) {
+    HIP_TRY(hipEventSynchronize(ev.back()));
+    for (int k = 0; k < FDLP_NUM_STAGES; ++k) {
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+      p->prof_ms[k] += ms;
+    }
+    p->prof_calls++;
+    for (auto e : ev) (void)hipEventDestroy(e);
+  }
+  p->prof_pending.clear();
+  return FDLP_OK;
+}
+
+int free_plan(fdlp_plan* p) {
+  if (!p) return FDLP_OK;
+  for (auto& ev : p->prof_pending)
+    for (auto e : ev) (void)hipEventDestroy(e);
+  void* devs[] = {p->d_fbank, p->d_hamming, p->d_weights, p->d_env_cos, p->d_env_win, p->d_tw1, p->d_post,
+                  p->d_om1, p->d_om2, p->d_lo, p->d_hi, p->ws.z, p->ws.dct, p->ws.r, p->ws.a, p->ws.gg,
+                  p->ws.cep, p->ws.env, p->d_frames, p->d_utts};
+  for (void* d : devs)
+    if (d) (void)hipFree(d);
+  if (p->h_frames) (void)hipHostFree(p->h_frames);
+  if (p->h_utts) (void)hipHostFree(p->h_utts);
+  if (p->staging_done) (void)hipEventDestroy(p->staging_done);
+  delete p;
+  return FDLP_OK;
+}
+
+template <typename T>
+int upload(T** dst, const T* src, size_t n) {
+  HIP_TRY(hipMalloc((void**)dst, sizeof(T) * std::max<size_t>(n, 1)));
+  if (n) HIP_TRY(hipMemcpy(*dst, src, sizeof(T) * n, hipMemcpyHostToDevice));
+  return FDLP_OK;
+}
+
+int64_t frames_of(const fdlp_plan* p, int64_t T) {
+  // getFrames: idx = sp_b + k*hop, yield while idx + sp_f < T + 2*ext  (features.py:151)
+  const int64_t lim = T + 2 * (int64_t)p->ext - p->sp_b - p->sp_f;  // k*hop < lim
+  if (lim <= 0) return 0;
+  return (lim - 1) / p->hop + 1;
+}
+
+int64_t out_of(const fdlp_plan* p, int64_t T) {
+  // int(np.ceil(T*frate/srate))  (computeFDLPSpectrogram.py:182)
+  return (int64_t)ceil((double)(T * (int64_t)p->cfg.frate) / (double)p->cfg.srate);
+}
+
+// OLA slices of computeFDLPSpectrogram.py:207-225 (see oracle.ola_plan for the numpy rules)
+int ola_table(const fdlp_plan* p, int F, int L, const uint8_t* jit, int32_t* dst, int32_t* src, int32_t* cnt) {
+  int64_t ptr = 0;
+  const int kk = p->kk, kkb2 = p->kkb2;
+  for (int i = 0; i < F; ++i) {
+    if (i == 0) {
+      if (L < kkb2) {
+        const int rhs = std::max(0, std::min(L, kk - kkb2));
+        if (rhs != L) return fail(FDLP_E_BROADCAST, "reference OLA would fail to broadcast (frame 0)");
+        dst[i] = 0; src[i] = kkb2; cnt[i] = L;
+      } else {
+        if (kk - kkb2 != kkb2) return fail(FDLP_E_BROADCAST, "reference OLA would fail to broadcast (frame 0)");
+        dst[i] = 0; src[i] = kkb2; cnt[i] = kkb2;
+      }
+    } else if (i == F - 1 || i == F - 2) {
+      const int64_t n = (int64_t)L - ptr;
+      if (kk >= n) {
+        const int64_t lhs = std::max<int64_t>(0, n);
+        const int64_t rhs = n >= 0 ? n : std::max<int64_t>(0, kk + n);
+        if (lhs != rhs) return fail(FDLP_E_BROADCAST, "reference OLA would fail to broadcast (tail frame)");
+        dst[i] = (int32_t)ptr; src[i] = 0; cnt[i] = (int32_t)lhs;
+      } else {
+        dst[i] = (int32_t)ptr; src[i] = 0; cnt[i] = kk;
+      }
+    } else {
+      if (ptr + kk > L) return fail(FDLP_E_BROADCAST, "reference OLA would fail to broadcast (middle frame)");
+      dst[i] = (int32_t)ptr; src[i] = 0; cnt[i] = kk;
+    }
+    if (i == 0) ptr = ptr + p->ola_hop - kkb2;
+    else ptr = ptr + p->ola_hop + (jit ? jit[i - 1] : 0);
+  }
+  return FDLP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fdlp_last_error(void) { return fdlp::last_error_slot().c_str(); }
+int fdlp_abi_version(void) { return FDLP_ABI_VERSION; }
+
+int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
+  if (!cfg || !out) return fail(FDLP_E_INVALID, "fdlp_plan_create: null argument");
+  *out = nullptr;
+  const fdlp_config& c = *cfg;
+  if (c.nfilters < 1 || c.order < 1 || c.coeff_num < 2 || c.srate < 1 || c.frate < 1 || !(c.fduration > 0))
+    return fail(FDLP_E_INVALID, "invalid configuration (nfilters>=1, order>=1, coeff_num>=2 required)");
+  if (c.max_frames < 1) return fail(FDLP_E_INVALID, "max_frames must be >= 1");
+  auto* p = new (std::nothrow) fdlp_plan;
+  if (!p) return fail(FDLP_E_NOMEM, "out of memory");
+  p->cfg = c;
+  p->cfg.lifter = nullptr;
+  p->device = device;
+  int rc;
+#define PLAN_FAIL(code, msg) do { rc = fail(code, msg); free_plan(p); return rc; } while (0)
+#define PLAN_TRY(expr) do { rc = (expr); if (rc != FDLP_OK) { std::string m_ = fdlp::last_error_slot(); free_plan(p); fdlp::last_error_slot() = m_; return rc; } } while (0)
+
+  // geometry, same float expressions as the reference
+  const double ov = 1.0 - c.overlap_fraction;                        // :104
+  p->N = (int)((double)c.srate * c.fduration);                       // features.py:134
+  const double lfr = 1.0 / (ov * c.fduration);                       // :174
+  p->hop = (int)((double)c.srate / lfr);                             // features.py:135
+  if (p->N % 2 == 0) { p->sp_b = p->N / 2 - 1; p->sp_f = p->N / 2; p->ext = p->N / 2 - 1; }
+  else { p->sp_b = p->sp_f = p->ext = (p->N - 1) / 2; }
+  p->nfft = (int)(2.0 * c.fduration * (double)c.srate);              // :53, :59
+  p->env_nfft = 2 * (int)(c.fduration * (double)c.frate);            // :201
+  p->kk = (int)nearbyint(c.fduration * (double)c.frate);             // :203 (np.round: half-even)
+  p->kkb2 = (int)nearbyint(c.fduration * (double)c.frate / 2.0);     // :204
+  p->ola_hop = (int)nearbyint(c.fduration * (double)c.frate * ov);   // :220
+  p->B = c.nfilters;
+  p->p = c.order;
+  p->M = c.coeff_num;
+  p->nlags = c.order + 2;
+  p->Me = std::min(p->M, p->env_nfft);
+  if (p->N < 2 || p->hop < 1) PLAN_FAIL(FDLP_E_INVALID, "frame length / hop too small");
+  if (p->kk < 1 || p->env_nfft < 1 || p->kk > p->env_nfft) PLAN_FAIL(FDLP_E_INVALID, "fduration*frate too small");
+  if (p->ola_hop < p->kkb2) PLAN_FAIL(FDLP_E_INVALID, "unsupported: negative OLA pointer (overlap too large)");
+  if (fdlp::autocorr_tiles(p->nlags) > 24) PLAN_FAIL(FDLP_E_INVALID, "order too large (max 366)");
+  if ((p->p + 1 + 63) / 64 > 6) PLAN_FAIL(FDLP_E_INVALID, "order too large for the Levinson kernel");
+  if (p->M > 4096) PLAN_FAIL(FDLP_E_INVALID, "coeff_num too large (max 4096)");
+  if (!split_four_step(p->N, &p->d1, &p->d2))
+    PLAN_FAIL(FDLP_E_INVALID, "frame length int(srate*fduration) has no supported 2/3/5/7 four-step split");
+
+  // filterbank (:49-63)
+  if (c.fbank_kind == FDLP_FBANK_MEL) {
+    p->fbank_host = fbank_mel(p->B, p->nfft, c.srate, c.warp_fact, &p->ncol);
+  } else if (c.fbank_kind == FDLP_FBANK_COCHLEAR) {
+    p->fbank_host = fbank_cochlear(p->B, p->nfft, c.srate, c.om_w, c.alp, c.fixed, c.bet, c.warp_fact, &p->ncol);
+  } else {
+    PLAN_FAIL(FDLP_E_INVALID, "Invalid type of filter bank, use mel or cochlear with proper configuration");
+  }
+  if (p->ncol - 1 != p->N)  // filt (ncol-1 taps) * cos_trans[i, :] (N) must broadcast (:190-191)
+    PLAN_FAIL(FDLP_E_INVALID, "filterbank width nfft/2 does not match the frame length (reference broadcast error)");
+  std::vector<double> dense((size_t)p->B * p->N);
+  p->lo.assign(p->B, 0);
+  p->hi.assign(p->B, 0);
+  for (int j = 0; j < p->B; ++j) {
+    const double* row = &p->fbank_host[(size_t)j * p->ncol];
+    double peak = 0.0;
+    for (int m = 0; m < p->N; ++m) peak = std::max(peak, std::fabs(row[m]));
+    const double thr = c.support_eps > 0 ? c.support_eps * peak : 0.0;
+    int lo = p->N, hi = 0;
+    for (int m = 0; m < p->N; ++m) {
+      dense[(size_t)j * p->N + m] = row[m];
+      const bool keep = c.support_eps > 0 ? std::fabs(row[m]) >= thr : row[m] != 0.0;
+      if (keep) { lo = std::min(lo, m); hi = m + 1; }
+    }
+    if (hi <= lo) { lo = 0; hi = 0; }
+    p->lo[j] = lo;
+    p->hi[j] = hi;
+  }
+
+  // modulation weights (:94-118)
+  const int M = p->M;
+  p->weights_host.assign((size_t)3 * M, 1.0);
+  for (int i = 0; i < M; ++i) p->weights_host[i] = (i >= c.coeff_lp && i <= c.coeff_hp) ? 1.0 : 0.0;
+  if (cfg->lifter) {
+    if (cfg->lifter_len != M) PLAN_FAIL(FDLP_E_INVALID, "lifter_config must hold coeff_num values (reference broadcast)");
+    for (int i = 0; i < M; ++i) p->weights_host[M + i] = cfg->lifter[i];
+  }
+  if (c.gamma_enabled) {
+    if (c.order != M) PLAN_FAIL(FDLP_E_INVALID, "gamma_weight has length order and needs order == coeff_num (reference broadcast)");
+    const std::vector<double> x = linspace(0.0, (double)(c.order - 1), c.order);  // :110
+    const double scale = c.gamma_scale, shape = c.gamma_shape;
+    const double pk_req = c.gamma_pk * (2.0 * c.fduration);                       // :114-115
+    const double pk = (shape - 1.0) * scale;                                      // :116
+    const double loc = -pk + pk_req;                                              // :117
+    for (int i = 0; i < M; ++i) p->weights_host[2 * M + i] = gamma_pdf(x[i], shape, loc, scale) * 3.0 * scale;
+  }
+
+  // windows and tables
+  const std::vector<double> ham = cos_window(p->N, 0.54, 0.46);
+  const std::vector<double> hann_k = cos_window(p->kk, 0.5, 0.5), hamm_k = cos_window(p->kk, 0.54, 0.46);
+  std::vector<double> env_win(2 * (size_t)p->kk);
+  for (int t = 0; t < p->kk; ++t) { env_win[2 * t] = hann_k[t]; env_win[2 * t + 1] = hamm_k[t]; }
+  std::vector<double> env_cos(p->env_nfft);
+  for (int q = 0; q < p->env_nfft; ++q)
+    env_cos[q] = (double)cosl(2.0L * (long double)M_PI * (long double)q / (long double)p->env_nfft);
+  const int N1 = p->d1.n, N2 = p->d2.n, N = p->N;
+  std::vector<double> tw1(2 * (size_t)N1 * N2), post(2 * (size_t)N);
+  const long double PI = 3.141592653589793238462643383279502884L;
+  for (int k1 = 0; k1 < N1; ++k1)
+    for (int n2 = 0; n2 < N2; ++n2) {
+      const long long q = ((long long)k1 * n2) % N;
+      const long double ang = -2.0L * PI * (long double)q / (long double)N;
+      tw1[2 * ((size_t)k1 * N2 + n2)] = (double)cosl(ang);
+      tw1[2 * ((size_t)k1 * N2 + n2) + 1] = (double)sinl(ang);
+    }
+  for (int k = 0; k < N; ++k) {
+    const long double ang = -PI * (long double)k / (2.0L * (long double)N);
+    post[2 * k] = (double)cosl(ang);
+    post[2 * k + 1] = (double)sinl(ang);
+  }
+  auto omega = [&](int n) {
+    std::vector<double2> om(n);
+    for (int q = 0; q < n; ++q) {
+      const long double ang = -2.0L * PI * (long double)q / (long double)n;
+      om[q] = make_double2((double)cosl(ang), (double)sinl(ang));
+    }
+    return om;
+  };
+  const std::vector<double2> om1 = omega(N1), om2 = omega(N2);
+
+  p->max_frames = c.max_frames;
+  if (device < 0) {  // host-only plan: geometry, filterbank, weights and OLA tables, no compute
+    *out = p;
+    return FDLP_OK;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) PLAN_FAIL(FDLP_E_HIP, "no HIP device visible");
+  if (device < 0 || device >= ndev) PLAN_FAIL(FDLP_E_INVALID, "device index out of range");
+  if (hipSetDevice(device) != hipSuccess) PLAN_FAIL(FDLP_E_HIP, "hipSetDevice failed");
+  PLAN_TRY(upload(&p->d_fbank, dense.data(), dense.size()));
+  PLAN_TRY(upload(&p->d_lo, p->lo.data(), p->lo.size()));
+  PLAN_TRY(upload(&p->d_hi, p->hi.data(), p->hi.size()));
+  PLAN_TRY(upload(&p->d_hamming, ham.data(), ham.size()));
+  PLAN_TRY(upload(&p->d_weights, p->weights_host.data(), p->weights_host.size()));
+  PLAN_TRY(upload(&p->d_env_cos, env_cos.data(), env_cos.size()));
+  PLAN_TRY(upload(&p->d_env_win, env_win.data(), env_win.size()));
+  PLAN_TRY(upload(&p->d_tw1, tw1.data(), tw1.size()));
+  PLAN_TRY(upload(&p->d_post, post.data(), post.size()));
+  PLAN_TRY(upload(&p->d_om1, om1.data(), om1.size()));
+  PLAN_TRY(upload(&p->d_om2, om2.data(), om2.size()));
+
+  fdlp::DevConsts& d = p->dc;
+  d.B = p->B; d.N = N; d.hop = p->hop; d.ext = p->ext; d.p = p->p; d.nlags = p->nlags; d.M = M; d.Me = p->Me;
+  d.kk = p->kk; d.env_nfft = p->env_nfft;
+  d.fbank = p->d_fbank; d.lo = p->d_lo; d.hi = p->d_hi; d.hamming = p->d_hamming; d.weights = p->d_weights;
+  d.env_cos = p->d_env_cos; d.env_win = p->d_env_win; d.tw1 = p->d_tw1; d.post = p->d_post;
+
+  // workspace
+  const size_t F = (size_t)c.max_frames, items = F * p->B;
+  p->max_frames = c.max_frames;
+  if (hipMalloc((void**)&p->ws.z, sizeof(double2) * F * N) != hipSuccess ||
+      hipMalloc((void**)&p->ws.dct, sizeof(double) * F * N) != hipSuccess ||
+      hipMalloc((void**)&p->ws.r, sizeof(double) * items * p->nlags) != hipSuccess ||
+      hipMalloc((void**)&p->ws.a, sizeof(double) * items * (p->p + 1)) != hipSuccess ||
+      hipMalloc((void**)&p->ws.gg, sizeof(double) * items) != hipSuccess ||
+      hipMalloc((void**)&p->ws.cep, sizeof(double) * items * M) != hipSuccess ||
+      hipMalloc((void**)&p->ws.env, sizeof(double) * items * p->kk) != hipSuccess ||
+      hipMalloc((void**)&p->d_frames, sizeof(fdlp::FrameDesc) * F) != hipSuccess ||
+      hipMalloc((void**)&p->d_utts, sizeof(fdlp::UttDesc) * F) != hipSuccess ||
+      hipHostMalloc((void**)&p->h_frames, sizeof(fdlp::FrameDesc) * F, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&p->h_utts, sizeof(fdlp::UttDesc) * F, hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&p->staging_done, hipEventDisableTiming) != hipSuccess)
+    PLAN_FAIL(FDLP_E_NOMEM, "workspace allocation failed (reduce max_frames)");
+#undef PLAN_FAIL
+#undef PLAN_TRY
+  *out = p;
+  return FDLP_OK;
+}
+
+int fdlp_plan_destroy(fdlp_plan* plan) {
+  if (plan && plan->device >= 0) (void)hipDeviceSynchronize();
+  return free_plan(plan);
+}
+
+int fdlp_geometry(const fdlp_plan* p, int64_t T, int32_t* F, int32_t* L) {
+  if (!p || T < 0) return fail(FDLP_E_INVALID, "fdlp_geometry: bad args");
+  if (F) *F = (int32_t)frames_of(p, T);
+  if (L) *L = (int32_t)out_of(p, T);
+  return FDLP_OK;
+}
+
+int fdlp_plan_info(const fdlp_plan* p, int32_t* N, int32_t* hop, int32_t* nlags, int32_t* kk, int32_t* ola_hop) {
+  if (!p) return fail(FDLP_E_INVALID, "fdlp_plan_info: null plan");
+  if (N) *N = p->N;
+  if (hop) *hop = p->hop;
+  if (nlags) *nlags = p->nlags;
+  if (kk) *kk = p->kk;
+  if (ola_hop) *ola_hop = p->ola_hop;
+  return FDLP_OK;
+}
+
+int fdlp_plan_fbank(const fdlp_plan* p, double* fbank_out, int32_t* lo, int32_t* hi) {
+  if (!p) return fail(FDLP_E_INVALID, "fdlp_plan_fbank: null plan");
+  if (fbank_out) memcpy(fbank_out, p->fbank_host.data(), sizeof(double) * p->fbank_host.size());
+  for (int j = 0; j < p->B; ++j) {
+    if (lo) lo[j] = p->lo[j];
+    if (hi) hi[j] = p->hi[j];
+  }
+  return FDLP_OK;
+}
+
+int fdlp_plan_weights(const fdlp_plan* p, double* w_out) {
+  if (!p || !w_out) return fail(FDLP_E_INVALID, "fdlp_plan_weights: bad args");
+  // folded product in the reference's multiplication order; odd zeroing applied after
+  for (int i = 0; i < p->M; ++i) {
+    double v = p->weights_host[i] * p->weights_host[p->M + i] * p->weights_host[2 * p->M + i];
+    if (p->cfg.odd_mod_zero && (i & 1)) v = 0.0;
+    w_out[i] = v;
+  }
+  return FDLP_OK;
+}
+
+int fdlp_ola_table(const fdlp_plan* p, int64_t T, const uint8_t* jitter, int32_t* dst, int32_t* src, int32_t* cnt) {
+  if (!p || !dst || !src || !cnt) return fail(FDLP_E_INVALID, "fdlp_ola_table: bad args");
+  return ola_table(p, (int)frames_of(p, T), (int)out_of(p, T), jitter, dst, src, cnt);
+}
+
+int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
+  if (!p || !b) return fail(FDLP_E_INVALID, "fdlp_compute: null argument");
+  if (b->n_utt < 0 || (b->n_utt > 0 && (!b->pcm_dev || !b->pcm_off || !b->utt_len || !b->out_row)))
+    return fail(FDLP_E_INVALID, "fdlp_compute: missing batch arrays");
+  if (b->pcm_kind != FDLP_PCM_I16 && b->pcm_kind != FDLP_PCM_F64) return fail(FDLP_E_INVALID, "bad pcm_kind");
+  if (b->noise_dev && (b->pcm_kind != FDLP_PCM_I16 || !b->noise_off || !b->noise_alpha))
+    return fail(FDLP_E_INVALID, "noise mixing needs int16 PCM, noise_off and noise_alpha");
+  if (!b->out_dev && !b->out_f64_dev) return fail(FDLP_E_INVALID, "fdlp_compute: no output buffer");
+  if (p->device < 0) return fail(FDLP_E_INVALID, "fdlp_compute: host-only plan (created with device < 0)");
+  hipStream_t s = (hipStream_t)stream;
+  int cur = -1;
+  if (hipGetDevice(&cur) == hipSuccess && cur != p->device) HIP_TRY(hipSetDevice(p->device));
+  // staging buffers may still feed the previous call's copies
+  if (p->staging_pending) {
+    HIP_TRY(hipEventSynchronize(p->staging_done));
+    p->staging_pending = false;
+  }
+  int64_t nf = 0;
+  int maxL = 0;
+  const uint8_t* jit = b->jitter;
+  std::vector<int32_t> dst, src, cnt;
+  for (int u = 0; u < b->n_utt; ++u) {
+    const int64_t T = b->utt_len[u];
+    const int64_t F = frames_of(p, T), L = out_of(p, T);
+    if (F < 1) return fail(FDLP_E_INVALID, "utterance too short: no analysis frame (scipy dct of an empty array)");
+    if (L > INT32_MAX / 2) return fail(FDLP_E_INVALID, "utterance too long");
+    if (nf + F > p->max_frames) return fail(FDLP_E_CAPACITY, "batch exceeds the plan's max_frames");
+    if (b->noise_dev && b->noise_off[u] < 0) return fail(FDLP_E_INVALID, "negative noise offset");
+    dst.resize(F); src.resize(F); cnt.resize(F);
+    int rc = ola_table(p, (int)F, (int)L, jit, dst.data(), src.data(), cnt.data());
+    if (rc != FDLP_OK) return rc;
+    if (jit) jit += F - 1;
+    for (int64_t k = 0; k < F; ++k) {
+      fdlp::FrameDesc& fd = p->h_frames[nf + k];
+      fd.pcm_off = b->pcm_off[u];
+      fd.noise_off = b->noise_dev ? b->noise_off[u] : -1;
+      fd.alpha = b->noise_dev ? b->noise_alpha[u] : 0.0;
+      fd.T = (int32_t)T;
+      fd.k = (int32_t)k;
+      fd.dst = dst[k]; fd.src = src[k]; fd.cnt = cnt[k];
+      fd.utt = u;
+    }
+    fdlp::UttDesc& ud = p->h_utts[u];
+    ud.out_row = b->out_row[u];
+    ud.L = (int32_t)L;
+    ud.frame0 = (int32_t)nf;
+    ud.F = (int32_t)F;
+    ud.pad = 0;
+    maxL = std::max(maxL, (int)L);
+    nf += F;
+  }
+  p->last_frames = (int)nf;
+  if (nf == 0) return FDLP_OK;
+  HIP_TRY(hipMemcpyAsync(p->d_frames, p->h_frames, sizeof(fdlp::FrameDesc) * nf, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(p->d_utts, p->h_utts, sizeof(fdlp::UttDesc) * b->n_utt, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipEventRecord(p->staging_done, s));
+  p->staging_pending = true;
+
+  const int items = (int)nf * p->B;
+  std::vector<hipEvent_t> ev;
+  if (p->profiling) {
+    if (p->prof_pending.size() >= 64) {
+      int rc = drain_profile(p);
+      if (rc != FDLP_OK) return rc;
+    }
+    ev.resize(FDLP_NUM_STAGES + 1);
+    for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+  }
+  auto mark = [&](int k) -> hipError_t { return p->profiling ? hipEventRecord(ev[k], s) : hipSuccess; };
+  HIP_TRY(mark(0));
+  HIP_TRY(fdlp::launch_frames_dft1(p->dc, p->d1, p->d2.n, b->pcm_dev, b->pcm_kind, b->noise_dev, p->d_frames,
+                                   nullptr, (int)nf, p->ws.z, p->d_om1, s));
+  HIP_TRY(mark(1));
+  HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z, (int)nf, p->ws.dct, p->d_om2, s));
+  HIP_TRY(mark(2));
+  HIP_TRY(fdlp::launch_autocorr(p->dc, p->ws.dct, nullptr, items, p->ws.r, s));
+  HIP_TRY(mark(3));
+  HIP_TRY(fdlp::launch_levinson(p->dc, p->ws.r, items, p->ws.a, p->ws.gg, s));
+  HIP_TRY(mark(4));
+  HIP_TRY(fdlp::launch_cepstrum(p->p, p->M, p->ws.a, p->ws.gg, items, p->ws.cep, s));
+  HIP_TRY(mark(5));
+  HIP_TRY(fdlp::launch_envelope(p->dc, p->cfg.odd_mod_zero, p->ws.cep, items, p->ws.env, s));
+  HIP_TRY(mark(6));
+  HIP_TRY(fdlp::launch_ola_log(p->dc, p->ws.env, p->d_frames, p->d_utts, b->n_utt, maxL, b->out_dev,
+                               b->out_f64_dev, b->ark_decimals, s));
+  HIP_TRY(mark(7));
+  if (p->profiling) p->prof_pending.push_back(ev);
+  return FDLP_OK;
+}
+
+int fdlp_set_profiling(fdlp_plan* p, int32_t enable) {
+  if (!p || p->device < 0) return fail(FDLP_E_INVALID, "fdlp_set_profiling: bad plan");
+  int rc = drain_profile(p);
+  if (rc != FDLP_OK) return rc;
+  p->profiling = enable != 0;
+  for (double& v : p->prof_ms) v = 0.0;
+  p->prof_calls = 0;
+  return FDLP_OK;
+}
+
+int fdlp_stage_times(fdlp_plan* p, double* ms_sum, int32_t* n_calls) {
+  if (!p || !ms_sum) return fail(FDLP_E_INVALID, "fdlp_stage_times: bad args");
+  int rc = drain_profile(p);
+  if (rc != FDLP_OK) return rc;
+  for (int k = 0; k < FDLP_NUM_STAGES; ++k) ms_sum[k] = p->prof_ms[k];
+  if (n_calls) *n_calls = p->prof_calls;
+  return FDLP_OK;
+}
+
+int fdlp_debug_fetch(fdlp_plan* p, int32_t n, double* dct, double* r, double* a, double* gg, double* cep,
+                     double* env) {
+  if (!p || n < 0 || n > p->max_frames || p->device < 0) return fail(FDLP_E_INVALID, "fdlp_debug_fetch: bad args");
+  HIP_TRY(hipDeviceSynchronize());
+  const size_t items = (size_t)n * p->B;
+  if (dct) HIP_TRY(hipMemcpy(dct, p->ws.dct, sizeof(double) * n * (size_t)p->N, hipMemcpyDeviceToHost));
+  if (r) HIP_TRY(hipMemcpy(r, p->ws.r, sizeof(double) * items * p->nlags, hipMemcpyDeviceToHost));
+  if (a) HIP_TRY(hipMemcpy(a, p->ws.a, sizeof(double) * items * (p->p + 1), hipMemcpyDeviceToHost));
+  if (gg) HIP_TRY(hipMemcpy(gg, p->ws.gg, sizeof(double) * items, hipMemcpyDeviceToHost));
+  if (cep) HIP_TRY(hipMemcpy(cep, p->ws.cep, sizeof(double) * items * p->M, hipMemcpyDeviceToHost));
+  if (env) HIP_TRY(hipMemcpy(env, p->ws.env, sizeof(double) * items * p->kk, hipMemcpyDeviceToHost));
+  return FDLP_OK;
+}
+
+int fdlp_dct_rows(fdlp_plan* p, const double* x, int32_t n, double* y, void* stream) {
+  if (!p || !x || !y || n < 0 || p->device < 0) return fail(FDLP_E_INVALID, "fdlp_dct_rows: bad args or host-only plan");
+  if (n > p->max_frames) return fail(FDLP_E_CAPACITY, "fdlp_dct_rows: more rows than max_frames");
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(fdlp::launch_frames_dft1(p->dc, p->d1, p->d2.n, nullptr, 0, nullptr, nullptr, x, n, p->ws.z, p->d_om1, s));
+  HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z, n, y, p->d_om2, s));
+  return FDLP_OK;
+}
+
+int fdlp_lpc_rows(fdlp_plan* p, const double* band, int32_t n, double* r, double* a, double* gg, void* stream) {
+  if (!p || !band || !r || !a || !gg || n < 0 || p->device < 0) return fail(FDLP_E_INVALID, "fdlp_lpc_rows: bad args or host-only plan");
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(fdlp::launch_autocorr(p->dc, nullptr, band, n, r, s));
+  HIP_TRY(fdlp::launch_levinson(p->dc, r, n, a, gg, s));
+  return FDLP_OK;
+}
+
+int fdlp_cepstrum_rows(fdlp_plan* p, const double* a, const double* gg, int32_t n, int32_t order, int32_t lim,
+                       double* cep, void* stream) {
+  if (!p || !a || !gg || !cep || n < 0 || order < 1 || lim < 2) return fail(FDLP_E_INVALID, "fdlp_cepstrum_rows: bad args");
+  HIP_TRY(fdlp::launch_cepstrum(order, lim, a, gg, n, cep, (hipStream_t)stream));
+  return FDLP_OK;
+}
+
+}  // extern "C"

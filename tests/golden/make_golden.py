@@ -1,0 +1,223 @@
+"""Generate the golden fixtures by running the REAL reference in the build container.
+
+Run once, here (the reference never travels to the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+It imports ``src/featgen/computeFDLPSpectrogram.py`` / ``features.py`` from the read-only
+reference tree, replaces ``dict2Ark`` (Kaldi ``copy-feats`` is absent here, and the real
+writer would silently write nothing: features.py:63-69) with a capture of the fp64 feature
+dict, seeds ``random`` (jitter, computeFDLPSpectrogram.py:225) and ``np.random`` (noise
+offset, features.py:25) right before each ``getFeats`` call, and stores inputs + outputs as
+small ``.npz`` fixtures next to this script.  Only data is stored (int16 inputs, fp64
+outputs, seeds, versions); no reference source.
+
+Inputs: seeded synthetic speech-like signals (AR(2)-coloured noise x syllabic envelope),
+white noise, edge lengths from SURVEY.md Appendix B, and two PESQ conformance clips shipped
+in the reference (e2e/reverb/local/PESQ_sources/P862/Software/Conform/*.wav, 8 kHz) upsampled
+2x to 16 kHz with scipy.signal.resample_poly and cropped.
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import tempfile
+from collections import OrderedDict
+
+import numpy as np
+import scipy
+from scipy.io import wavfile
+from scipy.signal import lfilter, resample_poly
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+PESQ_DIR = os.path.join(REF, "e2e/reverb/local/PESQ_sources/P862/Software/Conform")
+
+
+def speech_like(T, seed, rms=2000.0):
+    rng = np.random.default_rng(seed)
+    e = rng.standard_normal(T + 400)
+    # AR(2) resonance around 500-1500 Hz, random per utterance
+    f0 = rng.uniform(400, 1500)
+    rad = rng.uniform(0.90, 0.98)
+    a1, a2 = -2 * rad * np.cos(2 * np.pi * f0 / 16000), rad * rad
+    x = lfilter([1.0], [1.0, a1, a2], e)[400:]
+    t = np.arange(T) / 16000
+    env = 0.55 + 0.45 * np.sin(2 * np.pi * rng.uniform(3, 5) * t + rng.uniform(0, 6.28))
+    x = x * env
+    x = x / (np.sqrt(np.mean(x ** 2)) + 1e-12) * rms
+    return np.clip(np.round(x), -32768, 32767).astype(np.int16)
+
+
+def white(T, seed, scale=3000.0):
+    x = np.random.default_rng(seed).standard_normal(T) * scale
+    return np.clip(np.round(x), -32768, 32767).astype(np.int16)
+
+
+def pesq_clip(name, seconds):
+    sr, x = wavfile.read(os.path.join(PESQ_DIR, name))
+    assert sr == 8000
+    y = resample_poly(x.astype(np.float64), 2, 1)
+    y = np.clip(np.round(y), -32768, 32767).astype(np.int16)
+    return y[: int(seconds * 16000)]
+
+
+def run_reference(signals, opts, seed, noise_seed=None, noise=None, noise_name=None):
+    """Write WAVs + scp, call getFeats with an argparse Namespace, capture the dict."""
+    sys.path.insert(0, os.path.join(REF, "src/featgen"))
+    import computeFDLPSpectrogram as cf  # noqa: E402
+
+    captured = {}
+
+    def capture(feat_dict, outfile, kaldi_cmd):
+        captured.update({k: np.array(v) for k, v in feat_dict.items()})
+
+    cf.dict2Ark = capture
+    with tempfile.TemporaryDirectory() as td:
+        scp = os.path.join(td, "wav.scp")
+        with open(scp, "w") as f:
+            for utt, x in signals.items():
+                p = os.path.join(td, utt + ".wav")
+                wavfile.write(p, 16000, x)
+                f.write("%s %s\n" % (utt, p))
+        cwd = os.getcwd()
+        if noise is not None:
+            os.makedirs(os.path.join(td, "noises"), exist_ok=True)
+            wavfile.write(os.path.join(td, "noises", noise_name + ".wav"), 16000, noise)
+        os.chdir(td)
+        try:
+            ns = argparse.Namespace(
+                scp=scp, outfile=os.path.join(td, "out"), scp_type="wav",
+                nfilters=opts["nfilters"], coeff_num=opts["coeff_num"],
+                coeff_range=opts["coeff_range"], order=opts["order"],
+                fduration=opts["fduration"], frate=opts["frate"],
+                overlap_fraction=opts["overlap_fraction"], kaldi_cmd="true",
+                add_reverb=opts.get("add_reverb", "clean"), fbank_type=opts["fbank_type"],
+                odd_mod_zero=opts.get("odd_mod_zero", False),
+                gamma_weight=opts.get("gamma_weight", "None"),
+                lifter_config=opts.get("lifter_config"),
+                write_utt2num_frames=True, add_noise=opts.get("add_noise", "clean"))
+            random.seed(seed)
+            if noise_seed is not None:
+                np.random.seed(noise_seed)
+            cf.getFeats(ns)
+        finally:
+            os.chdir(cwd)
+    return captured
+
+
+WSJ = dict(nfilters=80, coeff_num=100, coeff_range="0,100", order=150, fduration=1.5,
+           frate=100, overlap_fraction=0.25, fbank_type="cochlear,1,1,1,2.5,1")
+REVERB = dict(WSJ, coeff_num=450, coeff_range="1,450")
+CHIME4 = dict(WSJ, coeff_range="1,100")
+CLI_DEFAULT = dict(nfilters=20, coeff_num=50, coeff_range="1,20", order=50, fduration=0.5,
+                   frate=100, overlap_fraction=0.25, fbank_type="mel,1")
+MEL80 = dict(WSJ, fbank_type="mel,1")
+
+
+def save(name, signals, opts, seed, feats, extra=None, more=None):
+    arrays = dict(more or {})
+    meta = dict(opts=opts, seed=seed, utts=list(signals.keys()),
+                numpy=np.__version__, scipy=scipy.__version__,
+                python=sys.version.split()[0], extra=extra or {})
+    for utt, x in signals.items():
+        arrays["in_" + utt] = x
+        arrays["out_" + utt] = feats[utt]
+    arrays["meta"] = np.array(json.dumps(meta))
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, sum(v.nbytes for v in arrays.values()) // 1024, "KiB raw")
+
+
+def stage_fixture():
+    """Per-stage intermediates for one frame x 3 bands (WSJ cfg), via reference primitives."""
+    sys.path.insert(0, os.path.join(REF, "src/featgen"))
+    import features as fe  # noqa: E402
+    import scipy.fftpack as fp
+    x = speech_like(30000, 11)
+    fr = np.array([f for f in fe.getFrames(x, 16000, 1 / (0.75 * 1.5), 1.5, np.hamming)])
+    dct = fp.dct(fr) / np.sqrt(2 * 24000)
+    fb = fe.createFbankCochlear(80, 48000, 16000, om_w=1.0, alp=1.0, fixed=1, bet=2.5, warp_fact=1.0)
+    fbm = fe.createFbank(80, 48000, 16000, warp_fact=1.0)
+    out = dict(x=x, frames0=fr[0], dct=dct, fb_rows=fb[[0, 37, 79]], fbm=fbm)
+    for tag, j in (("b0", 0), ("b37", 37), ("b79", 79)):
+        band = fb[j, :-1] * dct[1]
+        y = np.real(np.fft.ifft(np.fft.fft(band) * np.conj(np.fft.fft(band))))
+        a, gg = fe.computeLpcFast(band.copy(), 150)
+        cep100 = fe.computeModSpecFromLpc(gg, a.copy(), 100)
+        cep450 = fe.computeModSpecFromLpc(gg, a.copy(), 450)
+        out.update({tag + "_r": y[:152], tag + "_a": a, tag + "_gg": np.array(gg),
+                    tag + "_c100": cep100, tag + "_c450": cep450})
+    path = os.path.join(HERE, "stages_wsj.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path)
+
+
+def main():
+    os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
+    sys.dont_write_bytecode = True
+    stage_fixture()
+
+    wsj = OrderedDict()
+    wsj["short2"] = speech_like(2, 1)
+    wsj["s0p5"] = speech_like(8000, 2)
+    wsj["s1p0"] = speech_like(16000, 3)
+    wsj["s18000"] = speech_like(18000, 4)
+    wsj["s18002"] = speech_like(18002, 5)
+    wsj["s4p0"] = speech_like(64000, 6)
+    wsj["s4p5"] = speech_like(72000, 7)
+    wsj["white10"] = white(160000, 0)
+    wsj["pesq_or109"] = pesq_clip("or109.wav", 6.0)
+    wsj["pesq_u_af1s02"] = pesq_clip("u_af1s02.wav", 5.3)
+    save("wsj", wsj, WSJ, 1234, run_reference(wsj, WSJ, 1234))
+
+    rev = OrderedDict()
+    rev["r1p0"] = speech_like(16000, 21)
+    rev["r4p0"] = speech_like(64000, 22)
+    rev["pesq_dg149"] = pesq_clip("dg149.wav", 3.0)
+    save("reverb", rev, REVERB, 7, run_reference(rev, REVERB, 7))
+
+    noise = white(16000 * 20, 99, scale=2500.0)
+    noise[::7] = (noise[::7].astype(np.int32) * 3).clip(-32768, 32767).astype(np.int16)
+    ch = OrderedDict()
+    ch["c1"] = speech_like(40000, 31)
+    ch["c2"] = speech_like(27000, 32, rms=300.0)
+    ch["c3"] = speech_like(52000, 33)
+    opts = dict(CHIME4, add_noise="babble,20")
+    save("chime4_noise", ch, opts, 5, run_reference(ch, opts, 5, noise_seed=42, noise=noise,
+                                                    noise_name="babble"),
+         extra=dict(noise_seed=42), more=dict(noise_babble=noise))
+
+    cli = OrderedDict()
+    cli["m1"] = speech_like(20000, 41)
+    cli["m2"] = speech_like(35555, 42)
+    save("cli_default_mel", cli, CLI_DEFAULT, 3, run_reference(cli, CLI_DEFAULT, 3))
+
+    mel = OrderedDict()
+    mel["k1"] = speech_like(50000, 51)
+    save("mel80", mel, MEL80, 9, run_reference(mel, MEL80, 9))
+
+    dif = OrderedDict()
+    dif["d1"] = speech_like(30000, 61)
+    dif["d2"] = white(19000, 62)
+    opts = dict(WSJ, add_noise="diff")
+    save("wsj_diff", dif, opts, 11, run_reference(dif, opts, 11))
+
+    # gamma weight + odd-mod-zero + lifter file need p == M (computeFDLPSpectrogram.py:110,198)
+    with tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False) as f:
+        lif = np.round(1.0 + 0.5 * np.cos(np.arange(120) / 7.0), 6)
+        f.write(",".join("%.6f" % v for v in lif) + "\n")
+        lifpath = f.name
+    gw = OrderedDict()
+    gw["g1"] = speech_like(33000, 71)
+    opts = dict(WSJ, coeff_num=120, order=120, coeff_range="0,119", gamma_weight="20,1.5,3",
+                odd_mod_zero=True, lifter_config=lifpath)
+    feats = run_reference(gw, opts, 13)
+    opts = dict(opts, lifter_config=None)
+    save("gamma_lifter_odd", gw, opts, 13, feats, extra=dict(lifter=lif.tolist()))
+    os.unlink(lifpath)
+
+
+if __name__ == "__main__":
+    main()
