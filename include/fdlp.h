@@ -117,6 +117,9 @@ int fdlp_ola_table(const fdlp_plan* plan, int64_t T, const uint8_t* jitter, int3
 /* Whole pipeline for a batch (getFeats :159-229).  Enqueued on `stream`; host arrays are
  * consumed before return. */
 int fdlp_compute(fdlp_plan* plan, const fdlp_batch* batch, void* stream);
+/* Keep the fused LPC kernel's a/gg/cep in the workspace (off by default; needed by
+ * fdlp_debug_fetch for those three arrays). */
+int fdlp_set_debug(fdlp_plan* plan, int32_t keep_intermediates);
 /* Reads back the intermediates of the most recent fdlp_compute (parity/debug; synchronous):
  * any pointer may be NULL.  Layouts: dct [F,N]; r [F,B,nlags]; a [F,B,order+1]; gg [F,B];
  * cep [F,B,coeff_num]; env [F,B,kk]. */
@@ -124,9 +127,9 @@ int fdlp_debug_fetch(fdlp_plan* plan, int32_t n_frames, double* dct, double* r, 
                      double* gg, double* cep, double* env);
 
 /* Per-stage device time (HIP events on the compute stream) of every fdlp_compute since profiling
- * was (re)enabled.  Stages: 0 frames+column DFT, 1 row DFT+DCT, 2 autocorrelation, 3 Levinson,
- * 4 cepstrum, 5 envelope, 6 OLA+log.  fdlp_stage_times synchronises on the recorded events. */
-#define FDLP_NUM_STAGES 7
+ * was (re)enabled.  Stages: 0 frames+column DFT, 1 row DFT+DCT, 2 autocorrelation,
+ * 3 fused Levinson+cepstrum+envelope, 4 OLA+log.  fdlp_stage_times synchronises on the events. */
+#define FDLP_NUM_STAGES 5
 int fdlp_set_profiling(fdlp_plan* plan, int32_t enable);
 int fdlp_stage_times(fdlp_plan* plan, double* ms_sum /* [FDLP_NUM_STAGES] */, int32_t* n_calls);
 

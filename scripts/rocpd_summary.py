@@ -16,8 +16,8 @@ def main(db, out):
     pmc = {}
     try:
         for name, counter, val in c.execute(
-                "select k.name, p.counter_name, avg(p.value) from pmc_events p join kernels k "
-                "on p.event_id = k.id group by k.name, p.counter_name"):
+                "select kernel_name, counter_name, avg(value) from counters_collection "
+                "group by kernel_name, counter_name"):
             pmc.setdefault(name, {})[counter] = val
     except sqlite3.Error:
         pass

@@ -25,8 +25,8 @@ FDLP_FBANK_MEL = 0
 FDLP_FBANK_COCHLEAR = 1
 FDLP_PCM_I16 = 0
 FDLP_PCM_F64 = 1
-FDLP_NUM_STAGES = 7
-STAGE_NAMES = ("frames_dft1", "dft2_dct", "autocorr", "levinson", "cepstrum", "envelope", "ola_log")
+FDLP_NUM_STAGES = 5
+STAGE_NAMES = ("frames_dft1", "dft2_dct", "autocorr", "lpc_env", "ola_log")
 
 c_i32, c_i64, c_dbl, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 P_i32 = ctypes.POINTER(c_i32)
@@ -72,6 +72,7 @@ SIGNATURES = {
     "fdlp_compute": (c_i32, [c_p, ctypes.POINTER(FdlpBatchC), c_p]),
     "fdlp_debug_fetch": (c_i32, [c_p, c_i32, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl]),
     "fdlp_set_profiling": (c_i32, [c_p, c_i32]),
+    "fdlp_set_debug": (c_i32, [c_p, c_i32]),
     "fdlp_stage_times": (c_i32, [c_p, P_dbl, P_i32]),
     "fdlp_dct_rows": (c_i32, [c_p, c_p, c_i32, c_p, c_p]),
     "fdlp_lpc_rows": (c_i32, [c_p, c_p, c_i32, c_p, c_p, c_p, c_p]),

@@ -75,8 +75,9 @@ hipError_t launch_levinson(const DevConsts& c, const double* r, int items, doubl
                            double* gg, hipStream_t s);
 hipError_t launch_cepstrum(int p, int M, const double* a, const double* gg, int items,
                            double* cep, hipStream_t s);
-hipError_t launch_envelope(const DevConsts& c, int odd_zero, const double* cep, int items,
-                           double* env, hipStream_t s);
+hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int items, double* env,
+                          double* a_out, double* gg_out, double* cep_out, hipStream_t s);
+int lpc_env_region(int p, int M);
 int autocorr_tiles(int nlags);
 constexpr int kDftMaxSub = 512;  // longest LDS-resident sub-DFT of the four-step DCT
 hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc* frames,

@@ -12,9 +12,10 @@
 //   3. autocorr     : per (frame, band): x = W_j (.) D_f on the band's tap support, circular
 //                     autocorrelation lags 0..p+1 on MFMA f64 16x16x4 (lag-tiled Hankel GEMM,
 //                     DESIGN.md "autocorrelation as MFMA tiles").           (features.py:223-225)
-//   4. levinson     : one wave per (frame, band), Durbin recursion + gg.     (features.py:226-228)
-//   5. cepstrum     : one wave per item, LPC-cepstrum recursion, block-parallel. (features.py:233-246)
-//   6. envelope     : exp(Re DFT_{2*fd*fr}(c .* w))[0:kk] * hann/hamm.          (:194-205)
+//   4. lpc_env      : fused per (frame, band), 16 lanes per item: Durbin recursion + gg
+//                     (features.py:226-228) -> LPC cepstrum (features.py:233-246) -> weights ->
+//                     exp(Re DFT_{2*fd*fr}(c .* w))[0:kk] * hann/hamm (:194-205).
+//                     (levinson_kernel / cepstrum_kernel serve the per-stage entry points.)
 //   7. ola_log      : deterministic gather OLA + floor + log -> float32 [L, B].  (:207-229)
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -235,15 +236,22 @@ __global__ __launch_bounds__(256) void dft2_dct_kernel(DevConsts c, DftPlan d2, 
 // exactly one MFMA per tile per 64 positions.  r[l] = sum_i C_{t(i,l)}[i][(l+i) mod 16],
 // t(i,l) = (l+i) div 16.  Indices past N wrap (circular, features.py:223 uses FFTs of length N).
 // -----------------------------------------------------------------------------------------
-constexpr int kAcChunk = 1024;  // positions staged per LDS chunk
+// Staging: x = W_j (.) D_f is written into a mirrored LDS ring (every value at slot and
+// slot + kRing, so window reads never wrap) one 256-position chunk at a time; the D/W loads of
+// chunk c+2 are issued into registers before the MFMAs of chunk c and land in the ring after
+// them, so global latency hides behind 44 MFMAs per chunk.
+constexpr int kAcChunk = 256;   // positions per staged chunk (4 k-steps)
+constexpr int kAcRing = 512;    // ring holds chunks c and c+1 (the window halo of c is <= 16*NT <= 256)
+constexpr int kAcPer = kAcChunk / 64;
 
 template <int NT>
 __global__ __launch_bounds__(64) void autocorr_kernel(DevConsts c, const double* __restrict__ dct,
                                                       const double* __restrict__ dense,
                                                       double* __restrict__ rout) {
+  static_assert(16 * NT <= kAcChunk, "window halo must fit one chunk");
   constexpr int G = 4;                                  // tiles per epilogue group
   constexpr int kEpi = (16 * G + 15) * 17;              // padded lag-major epilogue buffer
-  constexpr int kStage = kAcChunk + 16 * NT;
+  constexpr int kStage = 2 * kAcRing;
   constexpr int kLds = kStage > kEpi ? kStage : kEpi;
   constexpr int NLPL = (16 * NT + 63) / 64;             // owned lags per lane
   __shared__ double xs[kLds];
@@ -274,25 +282,49 @@ __global__ __launch_bounds__(64) void autocorr_kernel(DevConsts c, const double*
 
   const int span = hi - lo;
   const int nsteps = (span + 63) / 64;
-  for (int s0 = 0; s0 < nsteps; s0 += kAcChunk / 64) {
-    const int steps = min(kAcChunk / 64, nsteps - s0);
-    const int base = lo + 64 * s0;
-    const int extent = 64 * steps + 16 * NT;
-    for (int q = lane; q < extent; q += 64) {
-      int pos = base + q;
-      while (pos >= N) pos -= N;  // circular
-      double v = 0.0;
-      if (pos >= lo && pos < hi) v = wrow ? wrow[pos] * drow[pos] : drow[pos];  // filt*dct (:191)
-      xs[q] = v;
+  const int nchunks = (nsteps + kAcPer - 1) / kAcPer;
+  double dv[kAcPer], wv[kAcPer];
+  // positions lo + 256*ch + 64*q + lane; indices past N wrap once (plan guarantees N >= 1024)
+  auto fetch = [&](int ch) {
+#pragma unroll
+    for (int q = 0; q < kAcPer; ++q) {
+      int pos = lo + kAcChunk * ch + 64 * q + lane;
+      if (pos >= N) pos -= N;
+      const bool ok = pos >= lo && pos < hi;
+      dv[q] = ok ? drow[pos] : 0.0;
+      wv[q] = ok ? (wrow ? wrow[pos] : 1.0) : 0.0;
     }
-    __syncthreads();
-    for (int s = 0; s < steps; ++s) {
-      const double* w = xs + 64 * s + 16 * kk_lane + i_lane;
+  };
+  auto store = [&](int ch) {
+#pragma unroll
+    for (int q = 0; q < kAcPer; ++q) {
+      const int slot = (kAcChunk * ch + 64 * q + lane) & (kAcRing - 1);
+      const double x = wv[q] * dv[q];  // filt * dct  (:191)
+      xs[slot] = x;
+      xs[slot + kAcRing] = x;
+    }
+  };
+  if (nsteps > 0) {
+    fetch(0);
+    store(0);
+    fetch(1);
+    store(1);
+    fetch(2);
+  }
+  __syncthreads();
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int s_end = min(kAcPer, nsteps - kAcPer * ch);
+    const int rbase = (kAcChunk * ch) & (kAcRing - 1);
+    for (int st = 0; st < s_end; ++st) {
+      const double* w = xs + rbase + 64 * st + 16 * kk_lane + i_lane;
       const double a = w[0];
 #pragma unroll
       for (int t = 0; t < NT; ++t)
         acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, w[16 * t], acc[t], 0, 0, 0);
     }
+    __syncthreads();
+    store(ch + 2);  // overwrites chunk ch's slots
+    if (ch + 3 <= nchunks) fetch(ch + 3);
     __syncthreads();
   }
 
@@ -347,57 +379,92 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // -----------------------------------------------------------------------------------------
+// 16-lane (one DPP row) helpers: an item is owned by a row of 16 lanes, 4 items per wave.
+// -----------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// sum over the 16 lanes of a DPP row; every lane gets the same (bitwise) value
+__device__ __forceinline__ double row_sum16(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x140>(v);  // row_mirror
+  return v;
+}
+__device__ __forceinline__ void wave_lds_sync() {
+  // LDS ops of one wave complete in order; this only stops the compiler from reordering
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// -----------------------------------------------------------------------------------------
 // 4. Levinson-Durbin (features.py:226-228): Toeplitz(r[0..p-1]) a' = -r[1..p]; a = [1, a'];
-//    gg = r0 + sum_{l=0}^{p} a_l r_{l+1}.  One wave per item, a[] distributed over lanes.
+//    gg = r0 + sum_{l=0}^{p} a_l r_{l+1}.  Four items per wave: an item's a[] is spread over a
+//    16-lane DPP row (lane l owns a_i, i = l + 16m); the per-order dot product is a 4-step DPP
+//    reduction and the reversed operand a_{k-i} comes from a per-row LDS mirror.
 // -----------------------------------------------------------------------------------------
 template <int SL>
-__global__ __launch_bounds__(64) void levinson_kernel(int p, int nlags, const double* __restrict__ r,
+__global__ __launch_bounds__(64) void levinson_kernel(int p, int nlags, int items, const double* __restrict__ r,
                                                       double* __restrict__ aout,
                                                       double* __restrict__ ggout) {
-  __shared__ double rs[64 * SL + 64];
-  __shared__ double as[64 * SL];
-  const int item = blockIdx.x;
-  const int lane = threadIdx.x;
-  for (int q = lane; q < 64 * SL + 64; q += 64) rs[q] = q < nlags ? r[(int64_t)item * nlags + q] : 0.0;
-  __syncthreads();
+  constexpr int RS = 16 * SL + 16;  // >= nlags
+  constexpr int AS = 16 * SL;
+  __shared__ double rs[4][RS];
+  __shared__ double as[4][AS];
+  const int g = threadIdx.x >> 4;
+  const int l = threadIdx.x & 15;
+  const int item = blockIdx.x * 4 + g;
+  const bool valid = item < items;
+  for (int q = l; q < RS; q += 16) rs[g][q] = (valid && q < nlags) ? r[(int64_t)item * nlags + q] : 0.0;
+  wave_lds_sync();
   double a[SL];
 #pragma unroll
-  for (int s = 0; s < SL; ++s) a[s] = (lane + 64 * s == 0) ? 1.0 : 0.0;
-  double E = rs[0];
+  for (int m = 0; m < SL; ++m) a[m] = (l + 16 * m == 0) ? 1.0 : 0.0;
+  double E = rs[g][0];
   for (int k = 1; k <= p; ++k) {
     double part = 0.0;
 #pragma unroll
-    for (int s = 0; s < SL; ++s) {
-      const int idx = lane + 64 * s;
-      if (idx >= 1 && idx < k) part += a[s] * rs[k - idx];
+    for (int m = 0; m < SL; ++m) {
+      const int i = l + 16 * m;
+      if (16 * m < k && i >= 1 && i < k) part += a[m] * rs[g][k - i];
     }
-    const double acc = rs[k] + wave_sum(part);
+    const double acc = rs[g][k] + row_sum16(part);
     const double kappa = -acc / E;
 #pragma unroll
-    for (int s = 0; s < SL; ++s) as[lane + 64 * s] = a[s];
-    __syncthreads();
+    for (int m = 0; m < SL; ++m)
+      if (16 * m < k) as[g][l + 16 * m] = a[m];
+    wave_lds_sync();
 #pragma unroll
-    for (int s = 0; s < SL; ++s) {
-      const int idx = lane + 64 * s;
-      if (idx >= 1 && idx < k) a[s] = a[s] + kappa * as[k - idx];
-      else if (idx == k) a[s] = kappa;
+    for (int m = 0; m < SL; ++m) {
+      const int i = l + 16 * m;
+      if (16 * m <= k) {
+        if (i >= 1 && i < k) a[m] = a[m] + kappa * as[g][k - i];
+        else if (i == k) a[m] = kappa;
+      }
     }
-    __syncthreads();
+    wave_lds_sync();
     E = E * (1.0 - kappa * kappa);
   }
   double part = 0.0;
 #pragma unroll
-  for (int s = 0; s < SL; ++s) {
-    const int idx = lane + 64 * s;
-    if (idx <= p) part += a[s] * rs[idx + 1];
+  for (int m = 0; m < SL; ++m) {
+    const int i = l + 16 * m;
+    if (i <= p) part += a[m] * rs[g][i + 1];
   }
-  const double gg = rs[0] + wave_sum(part);
+  const double gg = rs[g][0] + row_sum16(part);
+  if (valid) {
 #pragma unroll
-  for (int s = 0; s < SL; ++s) {
-    const int idx = lane + 64 * s;
-    if (idx <= p) aout[(int64_t)item * (p + 1) + idx] = a[s];
+    for (int m = 0; m < SL; ++m) {
+      const int i = l + 16 * m;
+      if (i <= p) aout[(int64_t)item * (p + 1) + i] = a[m];
+    }
+    if (l == 0) ggout[item] = gg;
   }
-  if (lane == 0) ggout[item] = gg;
 }
 
 // -----------------------------------------------------------------------------------------
@@ -455,40 +522,150 @@ __global__ __launch_bounds__(64) void cepstrum_kernel(int p, int M, const double
 }
 
 // -----------------------------------------------------------------------------------------
-// 6. envelope (computeFDLPSpectrogram.py:194-205):
-//    ms = c * mask [* lifter] [* gamma]; odd coefficients := 0; fft(ms, env_nfft) truncates or
-//    zero-pads; abs(exp(.)) = exp(Re); [0:kk] * hanning(kk) / hamming(kk).
+// 4-6 fused: Levinson -> gg -> LPC cepstrum -> modulation weights -> envelope, per (frame, band)
+// item, 16 lanes (one DPP row) per item, 4 items per wave.  Only r is read and only the kk
+// envelope samples are written (a/gg/cep optionally, for parity debugging).
+//   Levinson   features.py:226-228          cepstrum   features.py:233-246
+//   weights    computeFDLPSpectrogram.py:194-200
+//   envelope   computeFDLPSpectrogram.py:201-205: exp(Re sum_n c'_n cos(2 pi n t / env_nfft))
+//              * hanning(kk)[t] / hamming(kk)[t]  (fft(., env_nfft) truncates/zero-pads c')
+// Per-item LDS region (doubles): [a: NAL, zero beyond p][r: nlags, later c: M]; phase 3 reuses the
+// a slots for c'.  Envelope cosines come from a Chebyshev recurrence seeded with cos(2 pi t/env_nfft).
 // -----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void envelope_kernel(DevConsts c, int odd_zero, const double* __restrict__ cep,
-                                                      double* __restrict__ env) {
+struct LpcEnvArgs {
+  int p, nlags, M, Me, kk, env_nfft, odd_zero, items, region;
+  const double* r;
+  const double* weights;  // [3, M]
+  const double* env_cos;  // [env_nfft]
+  const double* env_win;  // [kk, 2]
+  double* env;            // [items, kk]
+  double* a_out;          // nullable [items, p+1]
+  double* gg_out;         // nullable [items]
+  double* cep_out;        // nullable [items, M]
+};
+
+// Durbin recursion with a[] resident in LDS (la[0..p], zero beyond) and r in LDS (lr): lane l of
+// the 16-lane row sums a_i r_{k-i} over i = l+1, l+17, ... and updates the symmetric pairs
+// (a_i, a_{k-i}) in place, so no mirror copy and no per-slot predicates are needed.  Returns gg.
+__device__ __forceinline__ double durbin16(double* la, const double* lr, int p, int l) {
+  double E = lr[0];
+  for (int k = 1; k <= p; ++k) {
+    double part = 0.0;
+    for (int i = l + 1; i < k; i += 16) part += la[i] * lr[k - i];
+    const double acc = lr[k] + row_sum16(part);
+    const double kappa = -acc / E;
+    wave_lds_sync();
+    for (int i = l + 1; 2 * i <= k; i += 16) {
+      const int j = k - i;
+      const double ai = la[i], aj = la[j];
+      if (i == j) {
+        la[i] = ai + kappa * ai;
+      } else {
+        la[i] = ai + kappa * aj;
+        la[j] = aj + kappa * ai;
+      }
+    }
+    if (l == 0) la[k] = kappa;
+    wave_lds_sync();
+    E = E * (1.0 - kappa * kappa);
+  }
+  double part = 0.0;
+  for (int i = l; i <= p; i += 16) part += la[i] * lr[i + 1];
+  return lr[0] + row_sum16(part);
+}
+
+template <int TS>
+__global__ __launch_bounds__(64) void lpc_env_kernel(LpcEnvArgs A) {
   extern __shared__ double sh[];
-  double* cw = sh;                  // [Me]
-  double* cq = sh + c.Me;           // [env_nfft]
-  const int item = blockIdx.x;
-  const int lane = threadIdx.x;
-  const double* mask = c.weights;
-  const double* lif = c.weights + c.M;
-  const double* gam = c.weights + 2 * c.M;
-  for (int n = lane; n < c.Me; n += 64) {
-    double v = cep[(int64_t)item * c.M + n];
-    v = v * mask[n];  // :194
-    v = v * lif[n];   // :195-196 (1.0 when absent: exact)
-    v = v * gam[n];   // :197-198 (1.0 when absent: exact)
-    if (odd_zero && (n & 1)) v = 0.0;  // :199-200 assignment (NaN-safe like the reference)
+  const int g = threadIdx.x >> 4;
+  const int l = threadIdx.x & 15;
+  const int item = blockIdx.x * 4 + g;
+  const bool valid = item < A.items;
+  const int p = A.p, nlags = A.nlags, M = A.M;
+  const int NAL = (M > p + 1 ? M : p + 1) + 16;
+  double* la = sh + g * A.region;  // a_0..a_p, zeros up to NAL (alpha = -a in phase 2)
+  double* lr = la + NAL;           // r (phase 1), then c (phase 2)
+  // ---- phase 1: Levinson-Durbin (features.py:226-228) ---------------------------------------
+  for (int q = l; q < nlags; q += 16) lr[q] = valid ? A.r[(int64_t)item * nlags + q] : 1.0;
+  for (int q = l; q < NAL; q += 16) la[q] = q == 0 ? 1.0 : 0.0;
+  wave_lds_sync();
+  const double gg = durbin16(la, lr, p, l);
+  if (valid && A.a_out) {
+    for (int i = l; i <= p; i += 16) A.a_out[(int64_t)item * (p + 1) + i] = la[i];
+    if (l == 0) A.gg_out[item] = gg;
+  }
+  wave_lds_sync();
+  // ---- phase 2: cepstrum (features.py:233-246), alpha_n = -la[n] --------------------------
+  double* cs = lr;
+  for (int b0 = 0; b0 < M; b0 += 16) {
+    const int n = b0 + l;
+    const double inv_n = 1.0 / (double)(n > 0 ? n : 1);
+    double acc = 0.0;
+    const int kstart = max(1, b0 - p);
+    double kd = (double)kstart;
+    for (int k = kstart; k < b0; ++k, kd += 1.0) acc -= ((kd * inv_n) * la[n - k]) * cs[k];
+    double mine = 0.0;
+    for (int kk = 0; kk < 16; ++kk) {
+      const int kg = b0 + kk;
+      if (kg >= M) break;
+      if (l == kk) {
+        if (kg == 0) mine = log(sqrt(gg));
+        else if (kg == 1) mine = -la[1];
+        else mine = acc - la[kg];
+      }
+      const double ck = __shfl(mine, (g << 4) + kk, 64);
+      if (kg >= 1 && l > kk) acc -= (((double)kg * inv_n) * la[n - kg]) * ck;
+    }
+    if (n < M) {
+      cs[n] = mine;
+      if (valid && A.cep_out) A.cep_out[(int64_t)item * M + n] = mine;
+    }
+    wave_lds_sync();
+  }
+  // ---- phase 3: weights + envelope (computeFDLPSpectrogram.py:194-205) ---------------------
+  double* cw = la;
+  const double* mask = A.weights;
+  const double* lif = A.weights + M;
+  const double* gam = A.weights + 2 * M;
+  for (int n = l; n < A.Me; n += 16) {
+    double v = cs[n];
+    v = v * mask[n];
+    v = v * lif[n];
+    v = v * gam[n];
+    if (A.odd_zero && (n & 1)) v = 0.0;
     cw[n] = v;
   }
-  for (int q = lane; q < c.env_nfft; q += 64) cq[q] = c.env_cos[q];
-  __syncthreads();
-  for (int t = lane; t < c.kk; t += 64) {
-    double s = 0.0;
-    int idx = 0;  // (n*t) mod env_nfft
-    for (int n = 0; n < c.Me; ++n) {
-      s += cw[n] * cq[idx];
-      idx += t;
-      if (idx >= c.env_nfft) idx -= c.env_nfft;
+  wave_lds_sync();
+  // sum_n cw_n cos(n theta_t) with the Chebyshev recurrence cos((n+1)t) = 2 cos t cos(nt) - cos((n-1)t)
+  double sum[TS], cprev[TS], ccur[TS], c2[TS];
+#pragma unroll
+  for (int q = 0; q < TS; ++q) {
+    const int t = l + 16 * q;
+    const double c1 = A.env_cos[t % A.env_nfft];
+    sum[q] = cw[0];
+    cprev[q] = 1.0;
+    ccur[q] = c1;
+    c2[q] = 2.0 * c1;
+  }
+  for (int n = 1; n < A.Me; ++n) {
+    const double w = cw[n];
+#pragma unroll
+    for (int q = 0; q < TS; ++q) {
+      sum[q] += w * ccur[q];
+      const double nxt = c2[q] * ccur[q] - cprev[q];
+      cprev[q] = ccur[q];
+      ccur[q] = nxt;
     }
-    const double e = exp(s);
-    env[(int64_t)item * c.kk + t] = (e * c.env_win[2 * t]) / c.env_win[2 * t + 1];
+  }
+  if (valid) {
+#pragma unroll
+    for (int q = 0; q < TS; ++q) {
+      const int t = l + 16 * q;
+      if (t < A.kk) {
+        const double e = exp(sum[q]);
+        A.env[(int64_t)item * A.kk + t] = (e * A.env_win[2 * t]) / A.env_win[2 * t + 1];
+      }
+    }
   }
 }
 
@@ -573,8 +750,7 @@ hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* 
     FDLP_AC_CASE(1) FDLP_AC_CASE(2) FDLP_AC_CASE(3) FDLP_AC_CASE(4) FDLP_AC_CASE(5)
     FDLP_AC_CASE(6) FDLP_AC_CASE(7) FDLP_AC_CASE(8) FDLP_AC_CASE(9) FDLP_AC_CASE(10)
     FDLP_AC_CASE(11) FDLP_AC_CASE(12) FDLP_AC_CASE(13) FDLP_AC_CASE(14) FDLP_AC_CASE(15)
-    FDLP_AC_CASE(16) FDLP_AC_CASE(17) FDLP_AC_CASE(18) FDLP_AC_CASE(19) FDLP_AC_CASE(20)
-    FDLP_AC_CASE(21) FDLP_AC_CASE(22) FDLP_AC_CASE(23) FDLP_AC_CASE(24)
+    FDLP_AC_CASE(16)
 #undef FDLP_AC_CASE
     default: return hipErrorInvalidValue;
   }
@@ -583,21 +759,19 @@ hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* 
 template <int SL>
 static hipError_t launch_lev_sl(int p, int nlags, const double* r, int items, double* a, double* gg,
                                 hipStream_t s) {
-  hipLaunchKernelGGL(levinson_kernel<SL>, dim3(items), dim3(64), 0, s, p, nlags, r, a, gg);
+  hipLaunchKernelGGL(levinson_kernel<SL>, dim3((items + 3) / 4), dim3(64), 0, s, p, nlags, items, r, a, gg);
   return hipGetLastError();
 }
 
 hipError_t launch_levinson(const DevConsts& c, const double* r, int items, double* a, double* gg,
                            hipStream_t s) {
   if (items <= 0) return hipSuccess;
-  const int sl = (c.p + 1 + 63) / 64;
-  switch (sl) {
-    case 1: return launch_lev_sl<1>(c.p, c.nlags, r, items, a, gg, s);
-    case 2: return launch_lev_sl<2>(c.p, c.nlags, r, items, a, gg, s);
-    case 3: return launch_lev_sl<3>(c.p, c.nlags, r, items, a, gg, s);
-    case 4: return launch_lev_sl<4>(c.p, c.nlags, r, items, a, gg, s);
-    case 5: return launch_lev_sl<5>(c.p, c.nlags, r, items, a, gg, s);
-    case 6: return launch_lev_sl<6>(c.p, c.nlags, r, items, a, gg, s);
+  switch ((c.p + 1 + 15) / 16) {
+#define FDLP_LEV_CASE(n) case n: return launch_lev_sl<n>(c.p, c.nlags, r, items, a, gg, s);
+    FDLP_LEV_CASE(1) FDLP_LEV_CASE(2) FDLP_LEV_CASE(3) FDLP_LEV_CASE(4) FDLP_LEV_CASE(5)
+    FDLP_LEV_CASE(6) FDLP_LEV_CASE(7) FDLP_LEV_CASE(8) FDLP_LEV_CASE(9) FDLP_LEV_CASE(10)
+    FDLP_LEV_CASE(11) FDLP_LEV_CASE(12) FDLP_LEV_CASE(13) FDLP_LEV_CASE(14) FDLP_LEV_CASE(15)
+#undef FDLP_LEV_CASE
     default: return hipErrorInvalidValue;
   }
 }
@@ -611,12 +785,36 @@ hipError_t launch_cepstrum(int p, int M, const double* a, const double* gg, int 
   return hipGetLastError();
 }
 
-hipError_t launch_envelope(const DevConsts& c, int odd_zero, const double* cep, int items, double* env,
-                           hipStream_t s) {
-  if (items <= 0) return hipSuccess;
-  size_t lds = sizeof(double) * (c.Me + c.env_nfft);
-  hipLaunchKernelGGL(envelope_kernel, dim3(items), dim3(64), lds, s, c, odd_zero, cep, env);
+template <int TS>
+static hipError_t launch_lpc_env_t(const LpcEnvArgs& A, size_t lds, hipStream_t s) {
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)lpc_env_kernel<TS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((lpc_env_kernel<TS>), dim3((A.items + 3) / 4), dim3(64), lds, s, A);
   return hipGetLastError();
+}
+
+int lpc_env_region(int p, int M) {
+  const int NAL = (M > p + 1 ? M : p + 1) + 16;
+  return NAL + (p + 2 > M ? p + 2 : M);
+}
+
+hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int items, double* env,
+                          double* a_out, double* gg_out, double* cep_out, hipStream_t s) {
+  if (items <= 0) return hipSuccess;
+  LpcEnvArgs A;
+  A.p = c.p; A.nlags = c.nlags; A.M = c.M; A.Me = c.Me; A.kk = c.kk; A.env_nfft = c.env_nfft;
+  A.odd_zero = odd_zero; A.items = items; A.region = lpc_env_region(c.p, c.M);
+  A.r = r; A.weights = c.weights; A.env_cos = c.env_cos; A.env_win = c.env_win; A.env = env;
+  A.a_out = a_out; A.gg_out = gg_out; A.cep_out = cep_out;
+  const size_t lds = sizeof(double) * (4 * (size_t)A.region);
+  switch ((c.kk + 15) / 16) {
+#define FDLP_TS_CASE(n) case n: return launch_lpc_env_t<n>(A, lds, s);
+    FDLP_TS_CASE(1) FDLP_TS_CASE(2) FDLP_TS_CASE(3) FDLP_TS_CASE(4) FDLP_TS_CASE(5) FDLP_TS_CASE(6)
+    FDLP_TS_CASE(7) FDLP_TS_CASE(8) FDLP_TS_CASE(9) FDLP_TS_CASE(10) FDLP_TS_CASE(11) FDLP_TS_CASE(12)
+    FDLP_TS_CASE(13) FDLP_TS_CASE(14) FDLP_TS_CASE(15) FDLP_TS_CASE(16)
+#undef FDLP_TS_CASE
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc* frames, const UttDesc* utts,

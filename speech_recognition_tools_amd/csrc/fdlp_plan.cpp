@@ -179,6 +179,7 @@ struct fdlp_plan {
   int last_frames = 0;
   // optional per-stage HIP-event timing (fdlp_set_profiling / fdlp_stage_times)
   bool profiling = false;
+  bool debug_intermediates = false;  // keep a/gg/cep of the fused LPC kernel for fdlp_debug_fetch
   std::vector<std::vector<hipEvent_t>> prof_pending;
   double prof_ms[FDLP_NUM_STAGES] = {0};
   int prof_calls = 0;
@@ -313,8 +314,10 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   if (p->N < 2 || p->hop < 1) PLAN_FAIL(FDLP_E_INVALID, "frame length / hop too small");
   if (p->kk < 1 || p->env_nfft < 1 || p->kk > p->env_nfft) PLAN_FAIL(FDLP_E_INVALID, "fduration*frate too small");
   if (p->ola_hop < p->kkb2) PLAN_FAIL(FDLP_E_INVALID, "unsupported: negative OLA pointer (overlap too large)");
-  if (fdlp::autocorr_tiles(p->nlags) > 24) PLAN_FAIL(FDLP_E_INVALID, "order too large (max 366)");
-  if ((p->p + 1 + 63) / 64 > 6) PLAN_FAIL(FDLP_E_INVALID, "order too large for the Levinson kernel");
+  if (fdlp::autocorr_tiles(p->nlags) > 16) PLAN_FAIL(FDLP_E_INVALID, "order too large (max 238)");
+  if (p->N < 1024) PLAN_FAIL(FDLP_E_INVALID, "frame length int(srate*fduration) must be >= 1024 samples");
+  if ((p->p + 1 + 15) / 16 > 15) PLAN_FAIL(FDLP_E_INVALID, "order too large for the Levinson kernel");
+  if (p->kk > 256) PLAN_FAIL(FDLP_E_INVALID, "fduration*frate too large (envelope > 256 samples)");
   if (p->M > 4096) PLAN_FAIL(FDLP_E_INVALID, "coeff_num too large (max 4096)");
   if (!split_four_step(p->N, &p->d1, &p->d2))
     PLAN_FAIL(FDLP_E_INVALID, "frame length int(srate*fduration) has no supported 2/3/5/7 four-step split");
@@ -573,16 +576,20 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
   HIP_TRY(mark(2));
   HIP_TRY(fdlp::launch_autocorr(p->dc, p->ws.dct, nullptr, items, p->ws.r, s));
   HIP_TRY(mark(3));
-  HIP_TRY(fdlp::launch_levinson(p->dc, p->ws.r, items, p->ws.a, p->ws.gg, s));
+  HIP_TRY(fdlp::launch_lpc_env(p->dc, p->cfg.odd_mod_zero, p->ws.r, items, p->ws.env,
+                               p->debug_intermediates ? p->ws.a : nullptr, p->debug_intermediates ? p->ws.gg : nullptr,
+                               p->debug_intermediates ? p->ws.cep : nullptr, s));
   HIP_TRY(mark(4));
-  HIP_TRY(fdlp::launch_cepstrum(p->p, p->M, p->ws.a, p->ws.gg, items, p->ws.cep, s));
-  HIP_TRY(mark(5));
-  HIP_TRY(fdlp::launch_envelope(p->dc, p->cfg.odd_mod_zero, p->ws.cep, items, p->ws.env, s));
-  HIP_TRY(mark(6));
   HIP_TRY(fdlp::launch_ola_log(p->dc, p->ws.env, p->d_frames, p->d_utts, b->n_utt, maxL, b->out_dev,
                                b->out_f64_dev, b->ark_decimals, s));
-  HIP_TRY(mark(7));
+  HIP_TRY(mark(5));
   if (p->profiling) p->prof_pending.push_back(ev);
+  return FDLP_OK;
+}
+
+int fdlp_set_debug(fdlp_plan* p, int32_t keep_intermediates) {
+  if (!p) return fail(FDLP_E_INVALID, "fdlp_set_debug: null plan");
+  p->debug_intermediates = keep_intermediates != 0;
   return FDLP_OK;
 }
 

@@ -14,7 +14,7 @@ import torch
 from . import _lib
 from ._lib import FdlpBatchC, FdlpConfigC, check, lib, ptr
 
-DEFAULT_SUPPORT_EPS = 1e-20
+DEFAULT_SUPPORT_EPS = 1e-12
 
 
 @dataclass
@@ -217,6 +217,9 @@ class FdlpPlan:
         s = stream if stream is not None else torch.cuda.current_stream(dev)
         check(lib.fdlp_compute(self._h, ctypes.byref(b), ctypes.c_void_p(s.cuda_stream)))
         return out[:total], rows, out64
+
+    def set_debug(self, keep_intermediates: bool = True):
+        check(lib.fdlp_set_debug(self._h, int(bool(keep_intermediates))))
 
     def debug_fetch(self, n_frames: int):
         F, B = int(n_frames), self.B

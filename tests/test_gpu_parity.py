@@ -42,10 +42,12 @@ def _batch_inputs(meta, sig, z):
     return pcm, kw
 
 
-def run_gpu(meta, sig, z, support_eps=None, max_frames=256):
+def run_gpu(meta, sig, z, support_eps=None, max_frames=256, debug=False):
     from speech_recognition_tools_amd import FdlpPlan, PyRandom
     cfg = feature_cfg(meta, support_eps)
     plan = FdlpPlan(cfg, device=0, max_frames=max_frames)
+    if debug:
+        plan.set_debug(True)
     utts = meta["utts"]
     lens = [sig[u].size for u in utts]
     nj = sum(max(plan.geometry(T)[0] - 1, 0) for T in lens)
@@ -71,7 +73,7 @@ def test_pipeline_vs_reference_golden(name):
         assert np.abs(f32 - q).max() <= max(1.0011e-3, 2 * TOL_UTT.get(u, 0)), (name, u)
 
 
-@pytest.mark.parametrize("eps", [0.0, 1e-12])
+@pytest.mark.parametrize("eps", [0.0, 1e-20, 1e-9])
 def test_support_eps_variants(eps):
     meta, sig, ref, z = load_golden("wsj")
     _, res = run_gpu(meta, sig, z, support_eps=eps)
@@ -124,7 +126,7 @@ def test_intermediates_vs_oracle():
     from oracle import fdlp_oracle as O
     meta, sig, ref, z = load_golden("wsj")
     sub = {"s4p0": sig["s4p0"]}
-    plan, res = run_gpu(dict(meta, utts=["s4p0"]), sub, z)
+    plan, res = run_gpu(dict(meta, utts=["s4p0"]), sub, z, debug=True)
     d = plan.debug_fetch(4)
     keep = O.Intermediates()
     O.FdlpOracle(oracle_cfg(meta)).band_envelopes(sig["s4p0"], keep)
