@@ -36,6 +36,7 @@ enum {
 
 enum { FDLP_FBANK_MEL = 0, FDLP_FBANK_COCHLEAR = 1 };
 enum { FDLP_PCM_I16 = 0, FDLP_PCM_F64 = 1 };
+enum { FDLP_PRE_NONE = 0, FDLP_PRE_DIFF = 1 };  /* --add_noise diff (computeFDLPSpectrogram.py:162-164) */
 
 /* Frozen feature configuration.  Mirrors the argparse surface of
  * computeFDLPSpectrogram.py:240-262 after the parsing getFeats does (:43-118). */
@@ -85,6 +86,8 @@ typedef struct fdlp_batch {
   double* out_f64_dev;           /* nullable device: same layout, fp64 log features (parity)     */
   int32_t ark_decimals;          /* >=0: round out_dev like '%.<d>f' text ark (dict2Ark
                                     features.py:66 uses 3); <0: keep full float32               */
+  int32_t preprocess;            /* FDLP_PRE_DIFF: x = convolve(int16 s, [1,2,3,2,0,-2,-5,-2,0,2,3,
+                                    2,1], 'same') on the device (int16 PCM only)                 */
 } fdlp_batch;
 
 /* ---- plan ------------------------------------------------------------------------------- */
@@ -105,6 +108,10 @@ int fdlp_plan_info(const fdlp_plan* plan, int32_t* N, int32_t* hop, int32_t* nla
 /* Host copy of the filterbank [nfilters, nfft/2+1] fp64 (createFbank / createFbankCochlear,
  * features.py:172-219) and of the per-band tap support [lo, hi). */
 int fdlp_plan_fbank(const fdlp_plan* plan, double* fbank_out, int32_t* lo, int32_t* hi);
+/* createFbank / createFbankCochlear (features.py:172-219) for an arbitrary nfft, using the
+ * fbank_kind / warp_fact / om_w / alp / fixed / bet / nfilters / srate fields of cfg.
+ * out: [nfilters, floor(nfft/2+1)]; *ncol receives the column count. */
+int fdlp_make_fbank(const fdlp_config* cfg, int32_t nfft, double* out, int32_t* ncol);
 /* Host copy of the folded modulation weights w[coeff_num] (:94-118, :194-200). */
 int fdlp_plan_weights(const fdlp_plan* plan, double* w_out);
 

@@ -1,0 +1,153 @@
+#!/usr/bin/env bash
+# Drop-in for recipes/timit/local_pyspeech/make_FDLPspectrum_feats.sh of
+# sadhusamik/speech_recognition_tools (same options and outputs), running each JOB's
+# compute-fdlp-feats on an MI355X.  Extra option: --ngpu N (JOBs are assigned round-robin to
+# GPUs 0..N-1 through HIP_VISIBLE_DEVICES; at most N JOBs run at once when no Kaldi $cmd is used).
+#
+#   make_FDLPspectrum_feats.sh [--opts] <data_dir> <feat_dir>
+# Inputs: <data_dir>/wav.scp or <data_dir>/segments.  Outputs: <data_dir>/feats.scp,
+# <data_dir>/utt2num_frames (with --write_utt2num_frames true), <feat_dir>/melspec_<name>.JOB.{ark,scp,len}.
+
+[ -f ./path.sh ] && . ./path.sh
+
+nj=100
+nfilters=20
+fduration=0.5
+coeff_num=50
+coeff_range='0,30'
+order=50
+overlap_fraction=0.25
+add_reverb=clean
+add_noise=clean
+fbank_type="mel,1"
+gamma_weight="None"
+odd_mod_zero=false
+frate=100
+cmd=
+add_opts=
+src_dir=
+spectrum_type=log
+write_utt2num_frames=false
+lifter_config=
+check_for_segment="data/train"
+ngpu=1
+seed=
+noise_seed=
+
+if [ -f utils/parse_options.sh ]; then
+  . utils/parse_options.sh || exit 1
+else
+  while [ $# -gt 0 ]; do
+    case "$1" in
+      --*=*) k="${1%%=*}"; k="${k#--}"; v="${1#*=}"; shift ;;
+      --*) k="${1#--}"; v="$2"; shift 2 ;;
+      *) break ;;
+    esac
+    k="${k//-/_}"
+    eval "$k=\"\$v\""
+  done
+fi
+
+here="$(cd "$(dirname "${BASH_SOURCE[0]}")/.." && pwd)"
+[ -z "$src_dir" ] && src_dir="$here/speech_recognition_tools_amd"
+cli="$src_dir/featgen/computeFDLPSpectrogram.py"
+
+if [ $# -ne 2 ]; then
+  echo "Usage: $0 [--opts] <data_dir> <feat_dir>"; exit 1
+fi
+data_dir=$1
+feat_dir=$2
+echo "$0 $@"
+case "$feat_dir" in /*) ;; *) feat_dir="$PWD/$feat_dir" ;; esac
+mkdir -p "$feat_dir"
+
+name=$(basename "$data_dir")
+scp=$data_dir/wav.scp
+segment=$data_dir/segments
+log_dir=$data_dir/log
+mkdir -p "$log_dir"
+
+$odd_mod_zero && add_opts="$add_opts --odd_mod_zero"
+$write_utt2num_frames && add_opts="$add_opts --write_utt2num_frames"
+[ -n "$lifter_config" ] && add_opts="$add_opts --lifter_config $lifter_config"
+[ -n "$seed" ] && add_opts="$add_opts --seed $seed"
+[ -n "$noise_seed" ] && add_opts="$add_opts --noise_seed $noise_seed"
+
+split_list() {  # split_list <in> <out1> ... : contiguous, balanced, like utils/split_scp.pl
+  local in=$1; shift
+  if [ -f utils/split_scp.pl ]; then utils/split_scp.pl "$in" "$@"; return $?; fi
+  python3 - "$in" "$@" <<'PY'
+import sys
+lines = open(sys.argv[1]).read().splitlines(True)
+outs = sys.argv[2:]
+n, k = len(lines), len(outs)
+if n < k:
+    sys.exit("split_scp: fewer lines (%d) than jobs (%d)" % (n, k))
+pos = 0
+for i, o in enumerate(outs):
+    m = n // k + (1 if i < n % k else 0)
+    open(o, "w").writelines(lines[pos:pos + m])
+    pos += m
+PY
+}
+
+run_jobs() {  # run_jobs <list-pattern containing JOB> <scp-type-opt>
+  local pattern=$1 stype=$2
+  if [ -n "$cmd" ]; then
+    $cmd JOB=1:$nj "$log_dir/feats_${name}.JOB.log" \
+      python3 "$cli" "$pattern" "$feat_dir/melspec_${name}.JOB" $add_opts $stype \
+        --fbank_type=$fbank_type --gamma_weight=$gamma_weight --add_reverb=$add_reverb \
+        --add_noise=$add_noise --coeff_num=$coeff_num --coeff_range=$coeff_range --order=$order \
+        --overlap_fraction=$overlap_fraction --nfilters=$nfilters --fduration=$fduration \
+        --frate=$frate || exit 1
+    return 0
+  fi
+  local pids=() n fail=0
+  for n in $(seq $nj); do
+    local g=$(( (n - 1) % ngpu ))
+    HIP_VISIBLE_DEVICES=$g python3 "$cli" "${pattern//JOB/$n}" "$feat_dir/melspec_${name}.$n" $add_opts $stype \
+      --fbank_type=$fbank_type --gamma_weight=$gamma_weight --add_reverb=$add_reverb \
+      --add_noise=$add_noise --coeff_num=$coeff_num --coeff_range=$coeff_range --order=$order \
+      --overlap_fraction=$overlap_fraction --nfilters=$nfilters --fduration=$fduration \
+      --frate=$frate > "$log_dir/feats_${name}.$n.log" 2>&1 &
+    pids+=($!)
+    if [ ${#pids[@]} -ge $ngpu ]; then
+      wait "${pids[0]}" || fail=1
+      pids=("${pids[@]:1}")
+    fi
+  done
+  for p in "${pids[@]}"; do wait "$p" || fail=1; done
+  [ $fail -eq 0 ] || { echo "$0: a JOB failed, see $log_dir/feats_${name}.*.log"; exit 1; }
+}
+
+if [ -f "$segment" ]; then
+  name_check=$(basename "$check_for_segment")
+  if [ -f "$check_for_segment/log/segment_dump/${name_check}_segmentdump.ark" ]; then
+    scp_dump_name=$check_for_segment/log/segment_dump/${name_check}_segmentdump
+  else
+    scp_dump_name=$log_dir/segment_dump/${name}_segmentdump
+    mkdir -p "$log_dir/segment_dump"
+    extract-segments scp,p:$scp $segment ark,scp:${scp_dump_name}.ark,${scp_dump_name}.scp || exit 1
+  fi
+  split_segments=""
+  for n in $(seq $nj); do split_segments="$split_segments $log_dir/segments.$n"; done
+  split_list ${scp_dump_name}.scp $split_segments || exit 1
+  run_jobs "$log_dir/segments.JOB" "--scp_type=segment"
+  for n in $(seq $nj); do cat "$feat_dir/melspec_$name.$n.scp" || exit 1; done > "$data_dir/feats.scp"
+  rm "$log_dir"/segments.*
+elif [ -f "$scp" ]; then
+  split_scp=""
+  for n in $(seq $nj); do split_scp="$split_scp $log_dir/wav_${name}.$n.scp"; done
+  split_list "$scp" $split_scp || exit 1
+  run_jobs "$log_dir/wav_${name}.JOB.scp" ""
+  for n in $(seq $nj); do cat "$feat_dir/melspec_$name.$n.scp" || exit 1; done > "$data_dir/feats.scp"
+  rm "$log_dir"/wav_${name}.*.scp
+else
+  echo "$0: Neither scp file nor segment file exists... something is wrong!"
+  exit 1
+fi
+
+if $write_utt2num_frames; then
+  for n in $(seq $nj); do cat "$feat_dir/melspec_$name.$n.len" || exit 1; done > "$data_dir/utt2num_frames"
+fi
+echo "$0: Finished computing FDLP spectrum features for $name"

@@ -25,6 +25,8 @@ FDLP_FBANK_MEL = 0
 FDLP_FBANK_COCHLEAR = 1
 FDLP_PCM_I16 = 0
 FDLP_PCM_F64 = 1
+FDLP_PRE_NONE = 0
+FDLP_PRE_DIFF = 1
 FDLP_NUM_STAGES = 5
 STAGE_NAMES = ("frames_dft1", "dft2_dct", "autocorr", "lpc_env", "ola_log")
 
@@ -54,7 +56,7 @@ class FdlpBatchC(ctypes.Structure):
         ("n_utt", c_i32), ("pcm_kind", c_i32), ("pcm_dev", c_p), ("pcm_off", P_i64),
         ("utt_len", P_i64), ("jitter", P_u8), ("noise_dev", c_p), ("noise_off", P_i64),
         ("noise_alpha", P_dbl), ("out_dev", c_p), ("out_row", P_i64), ("out_f64_dev", c_p),
-        ("ark_decimals", c_i32),
+        ("ark_decimals", c_i32), ("preprocess", c_i32),
     ]
 
 
@@ -68,6 +70,7 @@ SIGNATURES = {
     "fdlp_plan_info": (c_i32, [c_p, P_i32, P_i32, P_i32, P_i32, P_i32]),
     "fdlp_plan_fbank": (c_i32, [c_p, P_dbl, P_i32, P_i32]),
     "fdlp_plan_weights": (c_i32, [c_p, P_dbl]),
+    "fdlp_make_fbank": (c_i32, [ctypes.POINTER(FdlpConfigC), c_i32, P_dbl, P_i32]),
     "fdlp_ola_table": (c_i32, [c_p, c_i64, P_u8, P_i32, P_i32, P_i32]),
     "fdlp_compute": (c_i32, [c_p, ctypes.POINTER(FdlpBatchC), c_p]),
     "fdlp_debug_fetch": (c_i32, [c_p, c_i32, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl]),

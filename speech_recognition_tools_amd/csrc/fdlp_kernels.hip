@@ -127,6 +127,8 @@ __device__ __forceinline__ int64_t reflect_idx(int64_t q, int64_t T) {
   return q < T ? q : P - q;
 }
 
+__constant__ int kDiffTaps[13] = {1, 2, 3, 2, 0, -2, -5, -2, 0, 2, 3, 2, 1};  // :163
+
 __global__ __launch_bounds__(256) void frames_dft1_kernel(
     DevConsts c, DftPlan d1, int N2, const void* __restrict__ pcm, int pcm_kind,
     const int16_t* __restrict__ noise, const FrameDesc* __restrict__ frames,
@@ -165,8 +167,19 @@ __global__ __launch_bounds__(256) void frames_dft1_kernel(
             const double ns = (double)noise[fd.noise_off + t];
             s = __dadd_rn(s, __dmul_rn(fd.alpha, ns));
           }
-        } else {
+        } else if (pcm_kind == 1) {
           s = ((const double*)pcm)[fd.pcm_off + t];
+        } else {
+          // pcm_kind 2: scipy.signal.convolve(int16 s, diff kernel, 'same') -> int64, exact
+          // (computeFDLPSpectrogram.py:162-164); 'same' = full[6 : 6+T], zeros outside [0, T)
+          const int16_t* x = (const int16_t*)pcm + fd.pcm_off;
+          long long acc = 0;
+#pragma unroll
+          for (int q = 0; q < 13; ++q) {
+            const int64_t idx = t + 6 - q;
+            if (idx >= 0 && idx < fd.T) acc += (long long)kDiffTaps[q] * (long long)x[idx];
+          }
+          s = (double)acc;
         }
         val = __dmul_rn(s, c.hamming[m]);  // frame * win (features.py:153)
       }

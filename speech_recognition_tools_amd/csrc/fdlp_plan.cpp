@@ -483,6 +483,19 @@ int fdlp_plan_fbank(const fdlp_plan* p, double* fbank_out, int32_t* lo, int32_t*
   return FDLP_OK;
 }
 
+int fdlp_make_fbank(const fdlp_config* c, int32_t nfft, double* out, int32_t* ncol) {
+  if (!c || !out || nfft < 2 || c->nfilters < 1 || c->srate < 1) return fail(FDLP_E_INVALID, "fdlp_make_fbank: bad args");
+  int n = 0;
+  std::vector<double> W;
+  if (c->fbank_kind == FDLP_FBANK_MEL) W = fbank_mel(c->nfilters, nfft, c->srate, c->warp_fact, &n);
+  else if (c->fbank_kind == FDLP_FBANK_COCHLEAR)
+    W = fbank_cochlear(c->nfilters, nfft, c->srate, c->om_w, c->alp, c->fixed, c->bet, c->warp_fact, &n);
+  else return fail(FDLP_E_INVALID, "Invalid type of filter bank, use mel or cochlear with proper configuration");
+  memcpy(out, W.data(), sizeof(double) * W.size());
+  if (ncol) *ncol = n;
+  return FDLP_OK;
+}
+
 int fdlp_plan_weights(const fdlp_plan* p, double* w_out) {
   if (!p || !w_out) return fail(FDLP_E_INVALID, "fdlp_plan_weights: bad args");
   // folded product in the reference's multiplication order; odd zeroing applied after
@@ -506,6 +519,9 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
   if (b->pcm_kind != FDLP_PCM_I16 && b->pcm_kind != FDLP_PCM_F64) return fail(FDLP_E_INVALID, "bad pcm_kind");
   if (b->noise_dev && (b->pcm_kind != FDLP_PCM_I16 || !b->noise_off || !b->noise_alpha))
     return fail(FDLP_E_INVALID, "noise mixing needs int16 PCM, noise_off and noise_alpha");
+  if (b->preprocess != FDLP_PRE_NONE && b->preprocess != FDLP_PRE_DIFF) return fail(FDLP_E_INVALID, "bad preprocess");
+  if (b->preprocess == FDLP_PRE_DIFF && (b->pcm_kind != FDLP_PCM_I16 || b->noise_dev))
+    return fail(FDLP_E_INVALID, "diff preprocessing needs int16 PCM and no noise mixing");
   if (!b->out_dev && !b->out_f64_dev) return fail(FDLP_E_INVALID, "fdlp_compute: no output buffer");
   if (p->device < 0) return fail(FDLP_E_INVALID, "fdlp_compute: host-only plan (created with device < 0)");
   hipStream_t s = (hipStream_t)stream;
@@ -569,7 +585,8 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
   }
   auto mark = [&](int k) -> hipError_t { return p->profiling ? hipEventRecord(ev[k], s) : hipSuccess; };
   HIP_TRY(mark(0));
-  HIP_TRY(fdlp::launch_frames_dft1(p->dc, p->d1, p->d2.n, b->pcm_dev, b->pcm_kind, b->noise_dev, p->d_frames,
+  HIP_TRY(fdlp::launch_frames_dft1(p->dc, p->d1, p->d2.n, b->pcm_dev,
+                                   b->preprocess == FDLP_PRE_DIFF ? 2 : b->pcm_kind, b->noise_dev, p->d_frames,
                                    nullptr, (int)nf, p->ws.z, p->d_om1, s));
   HIP_TRY(mark(1));
   HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z, (int)nf, p->ws.dct, p->d_om2, s));

@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""compute-fdlp-feats: argv-compatible drop-in for
+sadhusamik/speech_recognition_tools src/featgen/computeFDLPSpectrogram.py (argparse :240-262,
+getFeats :29-237), running the FDLP pipeline on an MI355X through libfdlp_hip.so.
+
+Same positional arguments, options, defaults, outputs (<outfile>.ark/.scp[/.len]) and
+skip/abort semantics as the reference.  Differences (DESIGN.md "CLI"):
+  * the ark/scp are written natively in Kaldi binary format (no copy-feats; --kaldi_cmd is
+    accepted and ignored) with the reference's '%.3f' text-ark rounding (--ark_precision);
+  * --seed / --noise_seed make the hop jitter (random.randrange) and noise offsets
+    (np.random.rand) reproducible; unseeded runs draw seeds from os.urandom like the reference;
+  * a failure to write the ark exits non-zero (the reference ignores copy-feats' status).
+"""
+import argparse
+import os
+import subprocess
+import sys
+import time
+from collections import OrderedDict
+
+import numpy as np
+
+if __package__ in (None, ""):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+from speech_recognition_tools_amd.featgen import features  # noqa: E402
+from speech_recognition_tools_amd.featgen.features import (add_noise_to_wav_params, dict2Ark,  # noqa: E402
+                                                           load_noise, read_wav_bytes)
+
+
+def build_parser():
+    parser = argparse.ArgumentParser('Extract FDLP Spectrogram.')
+    parser.add_argument('scp', help='"scp" list')
+    parser.add_argument('outfile', help='output file')
+    parser.add_argument("--scp_type", default='wav', help="scp type can be 'wav' or 'segment'")
+    parser.add_argument('--nfilters', type=int, default=20, help='number of filters (15)')
+    parser.add_argument('--coeff_num', type=int, default=50, help='Total Number of coefficients to compute')
+    parser.add_argument('--coeff_range', type=str, default='1,20', help="Range of Modulation coefficients to keep")
+    parser.add_argument('--order', type=int, default=50, help='LPC filter order (50)')
+    parser.add_argument('--fduration', type=float, default=0.5, help='Window length (0.5 sec)')
+    parser.add_argument('--frate', type=int, default=100, help='Frame rate (100 Hz)')
+    parser.add_argument('--overlap_fraction', type=float, default=0.25, help='Fraction of Overlap for OLA')
+    parser.add_argument('--kaldi_cmd', default='copy-feats', help='Kaldi command to use to get ark files')
+    parser.add_argument('--add_reverb', help='input "clean" OR "small_room" OR "large_room"')
+    parser.add_argument('--fbank_type', type=str, default='mel,1',
+                        help='mel,warp_fact OR cochlear,om_w,alpa,fixed,beta,warp_fact')
+    parser.add_argument('--odd_mod_zero', action='store_true', help='Ignore the odd modulation coefficients')
+    parser.add_argument('--gamma_weight', type=str, default='None', help='Configured as scale,shape,pk')
+    parser.add_argument('--lifter_config', type=str, default=None, help='Configuration for general liftering')
+    parser.add_argument("--write_utt2num_frames", action="store_true", help="Set to write utt2num_frames")
+    parser.add_argument('--add_noise',
+                        help='Specify "type of noise, snr", types: babble, buccaneer1, buccaneer2, car, '
+                             'destroyerops, f16, factory1, factory2, m109, machinegun, pink, street, volvo, white')
+    # MI355X additions (all optional)
+    parser.add_argument('--seed', type=int, default=None, help='seed of the OLA hop jitter (random.seed)')
+    parser.add_argument('--noise_seed', type=int, default=None, help='seed of the noise offsets (np.random.seed)')
+    parser.add_argument('--device', type=int, default=None, help='HIP device (default: LOCAL_RANK or 0)')
+    parser.add_argument('--batch_frames', type=int, default=8192, help='analysis frames per GPU batch')
+    parser.add_argument('--ark_precision', type=int, default=3,
+                        help="decimals of the reference's text ark ('%%.3f'); -1 keeps full float32")
+    parser.add_argument('--support_eps', type=float, default=None,
+                        help='filter taps below eps*peak are skipped in the autocorrelation (0 = exact)')
+    return parser
+
+
+def _read_scp_entry(line, scp_type):
+    """(uttid, int16 samples, sr) or (uttid, None, None) on a read failure (skip, :129-154)."""
+    tokens = line.strip().split()
+    uttid, inwav = tokens[0], ' '.join(tokens[1:])
+    try:
+        if scp_type == 'wav':
+            if inwav[-1] == '|':                                            # :130-134
+                proc = subprocess.run(inwav[:-1], shell=True, stdout=subprocess.PIPE)
+                data = proc.stdout
+            else:                                                           # :138-139
+                with open(inwav, 'rb') as f:
+                    data = f.read()
+        elif scp_type == 'segment':                                         # :145-149
+            proc = subprocess.run('wav-copy ' + inwav + ' - ', shell=True, stdout=subprocess.PIPE)
+            data = proc.stdout
+        else:
+            raise ValueError('Invalid type of scp type, it should be either wav or segment')
+        sr, sig = read_wav_bytes(data)
+        return uttid, sig, sr
+    except ValueError as e:
+        if 'Invalid type of scp type' in str(e):
+            raise
+        return uttid, None, None
+    except Exception:
+        return uttid, None, None
+
+
+def getFeats(args, srate=16000, window=np.hamming):
+    """computeFDLPSpectrogram.py:29-237 on the device."""
+    if window is not np.hamming:
+        raise ValueError("only the reference's np.hamming analysis window is supported")
+    import torch
+    from speech_recognition_tools_amd import FdlpPlan, FeatureConfig, NpRandom, PyRandom
+
+    wavs, scp_type, outfile = args.scp, args.scp_type, args.outfile
+    add_noise, add_reverb = args.add_noise, args.add_reverb
+    cfg = FeatureConfig.from_args(args)                                     # :43-63 (+ValueErrors)
+    fbank_type = args.fbank_type.strip().split(',')
+    if fbank_type[0] == "cochlear" and int(fbank_type[3]) == 1:
+        print('%s: Alpha is fixed and will not change as a function of the center frequency...' % sys.argv[0])
+    if args.odd_mod_zero:
+        print('%s: Ignoring odd modulations... ' % sys.argv[0])
+    noise = None
+    diff = False
+    if add_noise:                                                           # :68-73
+        if add_noise == "clean" or add_noise == "diff":
+            print('%s: No noise added!' % sys.argv[0])
+            diff = add_noise == "diff"
+        else:
+            noise_info = add_noise.strip().split(',')
+            noise = load_noise(noise_info[0])
+            snr = float(noise_info[1])
+    if add_reverb:                                                          # :75-91
+        if add_reverb == 'clean':
+            print('%s: No reverberation added!' % sys.argv[0])
+        elif add_reverb in ('small_room', 'medium_room', 'large_room'):
+            raise NotImplementedError("--add_reverb %s (RIR convolution, features.py:110-115) is not ported yet"
+                                      % add_reverb)
+        else:
+            raise ValueError('Invalid type of reverberation!')
+    if not args.gamma_weight.strip().split(',')[0] == "None":
+        print('%s: Adding gamma filter on modulation frequencies...' % sys.argv[0])
+    if scp_type not in ('wav', 'segment'):
+        raise ValueError('Invalid type of scp type, it should be either wav or segment')
+
+    device = args.device if args.device is not None else int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(device)
+    plan = FdlpPlan(cfg, device=device, max_frames=max(int(args.batch_frames), 1))
+    jit_rng = PyRandom(args.seed)
+    noise_rng = NpRandom(args.noise_seed) if noise is not None else None
+    noise_dev = torch.from_numpy(np.ascontiguousarray(noise)).cuda(device) if noise is not None else None
+
+    all_feats = OrderedDict()
+    all_lens = OrderedDict()
+    pending = []  # (uttid, samples, F, noise_off, alpha)
+    pending_frames = 0
+
+    def flush():
+        nonlocal pending, pending_frames
+        if not pending:
+            return
+        lens = [x[1].shape[0] for x in pending]
+        jit = np.concatenate([jit_rng.randbits2(x[2] - 1) for x in pending])
+        pcm = np.concatenate([x[1] for x in pending])
+        kw = {}
+        if noise is not None:
+            kw = dict(noise=noise_dev, noise_off=[x[3] for x in pending], noise_alpha=[x[4] for x in pending])
+        out, rows, _ = plan.compute(torch.from_numpy(pcm).cuda(device), lens, jit, ark_decimals=args.ark_precision,
+                                    preprocess="diff" if diff else None, **kw)
+        host = out.cpu().numpy()
+        for i, x in enumerate(pending):
+            all_feats[x[0]] = host[rows[i]:rows[i + 1]]                   # :227
+            if args.write_utt2num_frames:
+                all_lens[x[0]] = int(rows[i + 1] - rows[i])               # :228-229
+        pending, pending_frames = [], 0
+
+    sr = None
+    with open(wavs, 'r') as fid:
+        for line in fid:                                                    # :125
+            if not line.strip():
+                continue
+            uttid, sig, sr_new = _read_scp_entry(line, scp_type)
+            skip = sig is None
+            if not skip:
+                sr = sr_new
+            if scp_type == 'wav':
+                if sr is None:  # the reference hits a NameError on 'sr' here (:144)
+                    raise NameError("name 'sr' is not defined")
+                assert sr == srate, 'Input file has different sampling rate.'  # :144
+            if skip:
+                continue
+            if sig.ndim != 1:
+                raise ValueError("multi-channel WAV input is not supported (the reference expects mono)")
+            T = sig.shape[0]
+            F, _ = plan.geometry(T)
+            if F < 1:
+                raise ValueError("invalid number of data points (0) specified")
+            off, alpha = 0, 0.0
+            if noise is not None:                                           # :166
+                off, alpha = add_noise_to_wav_params(sig, noise, snr, noise_rng.rand())
+            print('%s: Computing Features for file: %s' % (sys.argv[0], uttid))
+            sys.stdout.flush()
+            if pending_frames + F > plan.max_frames:
+                flush()
+            if F > plan.max_frames:
+                plan = FdlpPlan(cfg, device=device, max_frames=F)
+            pending.append((uttid, sig, F, off, alpha))
+            pending_frames += F
+    flush()
+    dict2Ark(all_feats, outfile, args.kaldi_cmd)                            # :231
+    if args.write_utt2num_frames:                                           # :232-237
+        with open(outfile + '.len', 'w+') as file:
+            for key, lens in all_lens.items():
+                file.write("{:s} {:d}".format(key, lens))
+                file.write("\n")
+    return all_feats
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    start_time = time.time()
+    print('%s: Extracting features....' % sys.argv[0])
+    sys.stdout.flush()
+    getFeats(args)
+    print('Execution Time: {t:.3f} seconds'.format(t=time.time() - start_time))
+    sys.stdout.flush()
+
+
+if __name__ == '__main__':
+    main()

@@ -164,7 +164,7 @@ class FdlpPlan:
                 offsets: Optional[Sequence[int]] = None, noise: Optional[torch.Tensor] = None,
                 noise_off: Optional[Sequence[int]] = None, noise_alpha: Optional[Sequence[float]] = None,
                 ark_decimals: int = 3, want_f64: bool = False, out: Optional[torch.Tensor] = None,
-                stream: Optional[torch.cuda.Stream] = None):
+                stream: Optional[torch.cuda.Stream] = None, preprocess: Optional[str] = None):
         """Features of a batch of utterances whose samples are concatenated in ``pcm`` (device).
 
         Returns (feats float32 [sum L, B], row offsets int64 [n_utt+1], feats_f64 or None)."""
@@ -214,6 +214,9 @@ class FdlpPlan:
         b.out_row = ptr(rows_c, ctypes.c_int64)
         b.out_f64_dev = out64.data_ptr() if out64 is not None else None
         b.ark_decimals = int(ark_decimals)
+        if preprocess not in (None, "diff"):
+            raise ValueError("preprocess must be None or 'diff'")
+        b.preprocess = _lib.FDLP_PRE_DIFF if preprocess == "diff" else _lib.FDLP_PRE_NONE
         s = stream if stream is not None else torch.cuda.current_stream(dev)
         check(lib.fdlp_compute(self._h, ctypes.byref(b), ctypes.c_void_p(s.cuda_stream)))
         return out[:total], rows, out64

@@ -154,9 +154,33 @@ def stage_fixture():
     print("wrote", path)
 
 
+def cli_options_fixture():
+    """The reference's argparse table (computeFDLPSpectrogram.py:240-261), read from its source
+    text with ast (names, defaults, types, actions) -> cli_options.json."""
+    import ast
+    src = open(os.path.join(REF, "src/featgen/computeFDLPSpectrogram.py")).read()
+    opts = []
+    for node in ast.walk(ast.parse(src)):
+        if isinstance(node, ast.Call) and getattr(node.func, "attr", "") == "add_argument":
+            name = ast.literal_eval(node.args[0])
+            kw = {}
+            for k in node.keywords:
+                if k.arg in ("default", "action"):
+                    kw[k.arg] = ast.literal_eval(k.value)
+                elif k.arg == "type":
+                    kw["type"] = k.value.id
+            opts.append(dict(name=name, **kw))
+    with open(os.path.join(HERE, "cli_options.json"), "w") as f:
+        json.dump(opts, f, indent=1)
+    print("wrote cli_options.json", len(opts))
+
+
 def main():
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
     sys.dont_write_bytecode = True
+    cli_options_fixture()
+    if "--cli-only" in sys.argv:
+        return
     stage_fixture()
 
     wsj = OrderedDict()
