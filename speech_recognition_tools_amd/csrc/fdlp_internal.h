@@ -79,6 +79,9 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
                           double* a_out, double* gg_out, double* cep_out, hipStream_t s);
 int lpc_env_region(int p, int M);
 int autocorr_tiles(int nlags);
+int band_fused_fits(int nlags, int p, int M, int kk);
+hipError_t launch_band_fused(const DevConsts& c, int odd_zero, const double* dct, int items, double* r_dbg,
+                             double* env, hipStream_t s);
 constexpr int kDftMaxSub = 512;  // longest LDS-resident sub-DFT of the four-step DCT
 hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc* frames,
                           const UttDesc* utts, int n_utt, int maxL, float* out,

@@ -12,7 +12,9 @@
 //   3. autocorr     : per (frame, band): x = W_j (.) D_f on the band's tap support, circular
 //                     autocorrelation lags 0..p+1 on MFMA f64 16x16x4 (lag-tiled Hankel GEMM,
 //                     DESIGN.md "autocorrelation as MFMA tiles").           (features.py:223-225)
-//   4. lpc_env      : fused per (frame, band), 16 lanes per item: Durbin recursion + gg
+//   3+4 band_fused  : autocorrelation followed, on the same wave, by Durbin + cepstrum + envelope
+//                     (64 lanes per item), so the VALU tail overlaps other waves' MFMAs.
+//   4. lpc_env      : (unfused alternative) per (frame, band), 16 lanes per item: Durbin + gg
 //                     (features.py:226-228) -> LPC cepstrum (features.py:233-246) -> weights ->
 //                     exp(Re DFT_{2*fd*fr}(c .* w))[0:kk] * hann/hamm (:194-205).
 //                     (levinson_kernel / cepstrum_kernel serve the per-stage entry points.)
@@ -20,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "fdlp_internal.h"
 
@@ -241,6 +244,144 @@ __global__ __launch_bounds__(256) void dft2_dct_kernel(DevConsts c, DftPlan d2, 
 }
 
 // -----------------------------------------------------------------------------------------
+// wave-level helpers
+// -----------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// -----------------------------------------------------------------------------------------
+// 16-lane (one DPP row) helpers: an item is owned by a row of 16 lanes, 4 items per wave.
+// -----------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// sum over the 16 lanes of a DPP row; every lane gets the same (bitwise) value
+__device__ __forceinline__ double row_sum16(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x140>(v);  // row_mirror
+  return v;
+}
+__device__ __forceinline__ void wave_lds_sync() {
+  // LDS ops of one wave complete in order; this only stops the compiler from reordering
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// -----------------------------------------------------------------------------------------
+// 64-lane (one item per wave) LPC tail used by the fused band kernel: Durbin, cepstrum and
+// envelope for ONE (frame, band) item right after its MFMA autocorrelation, so this VALU/LDS
+// work of one wave overlaps the MFMA phases of the other waves on the SIMD.
+// -----------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum64(double v) {
+  v = row_sum16(v);
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+struct LpcTail {
+  int p, nlags, M, Me, kk, odd_zero;
+  const double* weights;  // [3, M]
+  const double* env_cos;  // [env_nfft]
+  int env_nfft;
+  const double* env_win;  // [kk, 2]
+};
+
+constexpr int kTS64 = 4;  // envelope samples per lane (kk <= 256)
+
+// LDS: la[0..NAL) (a, zero beyond p), lr[0..max(nlags, M)) (r, then c).  Writes env[0..kk).
+__device__ void lpc_tail64(const LpcTail& T, double* la, double* lr, double* env, int lane) {
+  const int p = T.p, M = T.M;
+  // Durbin (features.py:226-228) with the symmetric in-place update (see durbin16)
+  double E = lr[0];
+  for (int k = 1; k <= p; ++k) {
+    double part = 0.0;
+    for (int i = lane + 1; i < k; i += 64) part += la[i] * lr[k - i];
+    const double acc = lr[k] + wave_sum64(part);
+    const double kappa = -acc / E;
+    wave_lds_sync();
+    for (int i = lane + 1; 2 * i <= k; i += 64) {
+      const int j = k - i;
+      const double ai = la[i], aj = la[j];
+      if (i == j) {
+        la[i] = ai + kappa * ai;
+      } else {
+        la[i] = ai + kappa * aj;
+        la[j] = aj + kappa * ai;
+      }
+    }
+    if (lane == 0) la[k] = kappa;
+    wave_lds_sync();
+    E = E * (1.0 - kappa * kappa);
+  }
+  double part = 0.0;
+  for (int i = lane; i <= p; i += 64) part += la[i] * lr[i + 1];
+  const double gg = lr[0] + wave_sum64(part);
+  wave_lds_sync();
+  // cepstrum (features.py:233-246), alpha_n = -a_n; c overwrites r
+  double* cs = lr;
+  for (int b0 = 0; b0 < M; b0 += 64) {
+    const int n = b0 + lane;
+    const double inv_n = 1.0 / (double)(n > 0 ? n : 1);
+    double acc = 0.0;
+    const int kstart = max(1, b0 - p);
+    double kd = (double)kstart;
+    if (n < M)
+      for (int k = kstart; k < b0; ++k, kd += 1.0) acc -= ((kd * inv_n) * la[n - k]) * cs[k];
+    double mine = 0.0;
+    for (int kk = 0; kk < 64; ++kk) {
+      const int kg = b0 + kk;
+      if (kg >= M) break;
+      if (lane == kk) {
+        if (kg == 0) mine = log(sqrt(gg));
+        else if (kg == 1) mine = -la[1];
+        else mine = acc - la[kg];
+      }
+      const double ck = __shfl(mine, kk, 64);
+      if (kg >= 1 && lane > kk && n < M) acc -= (((double)kg * inv_n) * la[n - kg]) * ck;
+    }
+    wave_lds_sync();
+    if (n < M) cs[n] = mine;
+    wave_lds_sync();
+  }
+  // weights + envelope (computeFDLPSpectrogram.py:194-205)
+  double* cw = la;
+  for (int n = lane; n < T.Me; n += 64) {
+    double v = cs[n];
+    v = v * T.weights[n];
+    v = v * T.weights[M + n];
+    v = v * T.weights[2 * M + n];
+    if (T.odd_zero && (n & 1)) v = 0.0;
+    cw[n] = v;
+  }
+  wave_lds_sync();
+  // one envelope sample at a time per lane keeps the tail's register footprint small (the
+  // MFMA accumulators of this kernel already hold 88 AGPRs)
+#pragma nounroll
+  for (int t = lane; t < T.kk; t += 64) {
+    const double c1 = T.env_cos[t % T.env_nfft];
+    const double c2 = 2.0 * c1;
+    double sum = cw[0], cprev = 1.0, ccur = c1;
+    for (int n = 1; n < T.Me; ++n) {
+      sum += cw[n] * ccur;
+      const double nxt = c2 * ccur - cprev;
+      cprev = ccur;
+      ccur = nxt;
+    }
+    env[t] = (exp(sum) * T.env_win[2 * t]) / T.env_win[2 * t + 1];
+  }
+}
+
+// -----------------------------------------------------------------------------------------
 // 3. circular autocorrelation, lags 0..nlags-1, on MFMA f64 16x16x4
 //
 // For one band signal x (support [lo,hi)), tile t (t = 0..NT-1) accumulates
@@ -257,12 +398,13 @@ constexpr int kAcChunk = 256;   // positions per staged chunk (4 k-steps)
 constexpr int kAcRing = 512;    // ring holds chunks c and c+1 (the window halo of c is <= 16*NT <= 256)
 constexpr int kAcPer = kAcChunk / 64;
 
-template <int NT>
-__global__ __launch_bounds__(64) void autocorr_kernel(DevConsts c, const double* __restrict__ dct,
+template <int NT, bool FUSE>
+__global__ __launch_bounds__(64, 4) void autocorr_kernel(DevConsts c, const double* __restrict__ dct,
                                                       const double* __restrict__ dense,
-                                                      double* __restrict__ rout) {
+                                                      double* __restrict__ rout, LpcTail tail,
+                                                      double* __restrict__ env) {
   static_assert(16 * NT <= kAcChunk, "window halo must fit one chunk");
-  constexpr int G = 4;                                  // tiles per epilogue group
+  constexpr int G = 2;                                  // tiles per epilogue group (LDS <= 8 KB)
   constexpr int kEpi = (16 * G + 15) * 17;              // padded lag-major epilogue buffer
   constexpr int kStage = 2 * kAcRing;
   constexpr int kLds = kStage > kEpi ? kStage : kEpi;
@@ -378,41 +520,170 @@ __global__ __launch_bounds__(64) void autocorr_kernel(DevConsts c, const double*
 #pragma unroll
   for (int q = 0; q < NLPL; ++q) {
     const int L = lane + 64 * q;
-    if (L < nlags) rout[(int64_t)item * nlags + L] = mine[q];
+    if (L < nlags && rout) rout[(int64_t)item * nlags + L] = mine[q];
+  }
+  if constexpr (FUSE) {
+    // LPC tail on the same wave (plan guarantees the region fits kLds)
+    const int NAL = (tail.M > tail.p + 1 ? tail.M : tail.p + 1) + 64;
+    double* la = xs;
+    double* lr = xs + NAL;
+    for (int q = lane; q < NAL; q += 64) la[q] = q == 0 ? 1.0 : 0.0;
+#pragma unroll
+    for (int q = 0; q < NLPL; ++q) {
+      const int L = lane + 64 * q;
+      if (L < nlags) lr[L] = mine[q];
+    }
+    wave_lds_sync();
+    lpc_tail64(tail, la, lr, env + (int64_t)item * tail.kk, lane);
   }
 }
 
-// -----------------------------------------------------------------------------------------
-// wave-level helpers
-// -----------------------------------------------------------------------------------------
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+template <int NT>
+constexpr int autocorr_lds_doubles() {
+  constexpr int kEpi = (16 * 4 + 15) * 17;
+  return 2 * kAcRing > kEpi ? 2 * kAcRing : kEpi;
 }
 
 // -----------------------------------------------------------------------------------------
-// 16-lane (one DPP row) helpers: an item is owned by a row of 16 lanes, 4 items per wave.
+// 3v. circular autocorrelation on the fp64 VALU (the default path).
+//
+// Measured on MI355X: v_fma_f64 sustains 75.8 TFLOP/s, v_mfma_f64_16x16x4f64 only ~51 TFLOP/s
+// (benchmarks/mfma_f64_peak.hip), and the MFMA lag tiling above wastes 13.6 % of its MACs, so a
+// register-blocked VALU kernel is the faster design for this fp64 path.
+// One wave per (frame, band).  Lane = (lag group g, slice s), g = lane>>3, s = lane&7: lanes own
+// LG consecutive lags [LG*g, LG*g+LG) and, in each 64-position super-block, the 8 positions
+// 8s..8s+7.  Per super-block a lane loads its 8 x[m] and the LG+7 window values x[m+LG*g+...]
+// from the LDS ring and issues 8*LG FMAs (152 FMAs per 34 LDS reads for p = 150).  The 8 slices of a
+// lag group are summed with DPP at the end.
 // -----------------------------------------------------------------------------------------
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-// sum over the 16 lanes of a DPP row; every lane gets the same (bitwise) value
-__device__ __forceinline__ double row_sum16(double v) {
+__device__ __forceinline__ double sum8(double v) {  // over the 8 lanes of a half DPP row
   v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp_f64<0x141>(v);  // row_half_mirror
-  v += dpp_f64<0x140>(v);  // row_mirror
+  v += dpp_f64<0x141>(v);  // row_half_mirror: lane i <-> 7-i inside each 8-lane half
   return v;
 }
-__device__ __forceinline__ void wave_lds_sync() {
-  // LDS ops of one wave complete in order; this only stops the compiler from reordering
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+// LDS read of one double at a compile-time byte offset from a per-lane byte address.  Plain
+// ds_read_b64 (2 LDS cycles per wave when conflict-free); the compiler would otherwise merge the
+// window into ds_read2_b64 / ds_read_b128, which run at half rate or 2-way conflicted here.
+// The caller waits with lds_wait() before using the values.
+template <int OFF>
+__device__ __forceinline__ double lds_ld(uint32_t addr) {
+  double v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <int MB, int WIN, int Q = 0>
+__device__ __forceinline__ void load_window(double* a, double* b, uint32_t xa, uint32_t wa) {
+  if constexpr (Q < MB) a[Q] = lds_ld<8 * Q>(xa);
+  if constexpr (Q < WIN) b[Q] = lds_ld<8 * Q>(wa);
+  if constexpr (Q + 1 < (MB > WIN ? MB : WIN)) load_window<MB, WIN, Q + 1>(a, b, xa, wa);
+}
+
+template <int LG>
+__global__ __launch_bounds__(64, 4) void autocorr_valu_kernel(DevConsts c, const double* __restrict__ dct,
+                                                              const double* __restrict__ dense,
+                                                              double* __restrict__ rout) {
+  constexpr int MB = 8;                 // positions per lane per super-block
+  constexpr int WIN = MB + LG - 1;      // window values per lane
+  static_assert(8 * LG + 64 <= kAcChunk + 64, "window halo must fit one chunk");
+  __shared__ double xs[2 * kAcRing];
+
+  const int item = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int N = c.N;
+  int lo, hi;
+  const double* drow;
+  const double* wrow = nullptr;
+  if (dense) {
+    lo = 0;
+    hi = N;
+    drow = dense + (int64_t)item * N;
+  } else {
+    const int f = item / c.B, j = item % c.B;
+    lo = c.lo[j];
+    hi = c.hi[j];
+    drow = dct + (int64_t)f * N;
+    wrow = c.fbank + (int64_t)j * N;
+  }
+  // lane -> (lag group g, slice sl): slices 0-3 in lanes 0-31 and 4-7 in lanes 32-63, so each
+  // 32-lane LDS service group reads 32 distinct banks for odd LG (offsets 8*sl + LG*g mod 32).
+  const int sl = (lane & 3) + 4 * (lane >> 5);
+  const int g = (lane >> 2) & 7;
+  double acc[LG];
+#pragma unroll
+  for (int q = 0; q < LG; ++q) acc[q] = 0.0;
+
+  const int span = hi - lo;
+  const int nsb = (span + 63) / 64;                     // super-blocks of 64 positions
+  const int nchunks = (nsb + kAcPer - 1) / kAcPer;
+  double dv[kAcPer], wv[kAcPer];
+  auto fetch = [&](int ch) {
+#pragma unroll
+    for (int q = 0; q < kAcPer; ++q) {
+      int pos = lo + kAcChunk * ch + 64 * q + lane;
+      if (pos >= N) pos -= N;
+      const bool ok = pos >= lo && pos < hi;
+      dv[q] = ok ? drow[pos] : 0.0;
+      wv[q] = ok ? (wrow ? wrow[pos] : 1.0) : 0.0;
+    }
+  };
+  auto store = [&](int ch) {
+#pragma unroll
+    for (int q = 0; q < kAcPer; ++q) {
+      const int slot = (kAcChunk * ch + 64 * q + lane) & (kAcRing - 1);
+      const double x = wv[q] * dv[q];  // filt * dct  (:191)
+      xs[slot] = x;
+      xs[slot + kAcRing] = x;
+    }
+  };
+  if (nsb > 0) {
+    fetch(0);
+    store(0);
+    fetch(1);
+    store(1);
+    fetch(2);
+  }
+  __syncthreads();
+  // 32-bit LDS byte address of xs (address space 3), as ds_read expects
+  const uint32_t xs_addr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) double*)xs);
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int sb_end = min(kAcPer, nsb - kAcPer * ch);
+    const int rbase = (kAcChunk * ch) & (kAcRing - 1);
+    for (int sb = 0; sb < sb_end; ++sb) {
+      const uint32_t xa = xs_addr + 8u * (uint32_t)(rbase + 64 * sb + MB * sl);
+      const uint32_t wa = xa + 8u * (uint32_t)(LG * g);
+      double a[MB], b[WIN];
+      load_window<MB, WIN>(a, b, xa, wa);
+      lds_wait();
+      // pin every loaded value behind the wait: the compiler does not know the asm loads are
+      // asynchronous, so no use (or copy) of a/b may be scheduled before lgkmcnt(0)
+#pragma unroll
+      for (int q = 0; q < MB; ++q) asm volatile("" : "+v"(a[q]));
+#pragma unroll
+      for (int q = 0; q < WIN; ++q) asm volatile("" : "+v"(b[q]));
+#pragma unroll
+      for (int q = 0; q < MB; ++q)
+#pragma unroll
+        for (int t = 0; t < LG; ++t) acc[t] = fma(a[q], b[q + t], acc[t]);
+    }
+    __syncthreads();
+    store(ch + 2);
+    if (ch + 3 <= nchunks) fetch(ch + 3);
+    __syncthreads();
+  }
+  const int nlags = c.nlags;
+#pragma unroll
+  for (int t = 0; t < LG; ++t) {
+    double v = acc[t];
+    v += dpp_f64<0xB1>(v);  // quad: lanes 4g..4g+3 hold slices 0-3 (or 4-7)
+    v += dpp_f64<0x4E>(v);
+    v += __shfl_xor(v, 32, 64);
+    const int L = LG * g + t;
+    if (lane < 32 && (lane & 3) == 0 && L < nlags) rout[(int64_t)item * nlags + L] = v;
+  }
 }
 
 // -----------------------------------------------------------------------------------------
@@ -748,18 +1019,29 @@ hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const 
 
 template <int NT>
 static hipError_t launch_ac_nt(const DevConsts& c, const double* dct, const double* dense, int items,
-                               double* r, hipStream_t s) {
-  hipLaunchKernelGGL(autocorr_kernel<NT>, dim3(items), dim3(64), 0, s, c, dct, dense, r);
+                               double* r, const LpcTail* tail, double* env, hipStream_t s) {
+  if (tail) {
+    hipLaunchKernelGGL((autocorr_kernel<NT, true>), dim3(items), dim3(64), 0, s, c, dct, dense, r, *tail, env);
+  } else {
+    LpcTail none{};
+    hipLaunchKernelGGL((autocorr_kernel<NT, false>), dim3(items), dim3(64), 0, s, c, dct, dense, r, none, env);
+  }
   return hipGetLastError();
 }
 
 int autocorr_tiles(int nlags) { return ((nlags + 14) >> 4) + 1; }
 
-hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* dense, int items,
-                           double* r, hipStream_t s) {
+int band_fused_fits(int nlags, int p, int M, int kk) {
+  const int NAL = (M > p + 1 ? M : p + 1) + 64;
+  const int need = NAL + (nlags > M ? nlags : M);
+  return need <= (16 * 4 + 15) * 17 && kk <= 64 * kTS64;
+}
+
+static hipError_t launch_autocorr_any(const DevConsts& c, const double* dct, const double* dense, int items,
+                                      double* r, const LpcTail* tail, double* env, hipStream_t s) {
   if (items <= 0) return hipSuccess;
   switch (autocorr_tiles(c.nlags)) {
-#define FDLP_AC_CASE(n) case n: return launch_ac_nt<n>(c, dct, dense, items, r, s);
+#define FDLP_AC_CASE(n) case n: return launch_ac_nt<n>(c, dct, dense, items, r, tail, env, s);
     FDLP_AC_CASE(1) FDLP_AC_CASE(2) FDLP_AC_CASE(3) FDLP_AC_CASE(4) FDLP_AC_CASE(5)
     FDLP_AC_CASE(6) FDLP_AC_CASE(7) FDLP_AC_CASE(8) FDLP_AC_CASE(9) FDLP_AC_CASE(10)
     FDLP_AC_CASE(11) FDLP_AC_CASE(12) FDLP_AC_CASE(13) FDLP_AC_CASE(14) FDLP_AC_CASE(15)
@@ -767,6 +1049,46 @@ hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* 
 #undef FDLP_AC_CASE
     default: return hipErrorInvalidValue;
   }
+}
+
+template <int LG>
+static hipError_t launch_acv_lg(const DevConsts& c, const double* dct, const double* dense, int items, double* r,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(autocorr_valu_kernel<LG>, dim3(items), dim3(64), 0, s, c, dct, dense, r);
+  return hipGetLastError();
+}
+
+int autocorr_valu_lags_per_group(int nlags) { return (nlags + 7) / 8; }
+
+hipError_t launch_autocorr_valu(const DevConsts& c, const double* dct, const double* dense, int items, double* r,
+                                hipStream_t s) {
+  if (items <= 0) return hipSuccess;
+  switch (autocorr_valu_lags_per_group(c.nlags)) {
+#define FDLP_ACV_CASE(n) case n: return launch_acv_lg<n>(c, dct, dense, items, r, s);
+    FDLP_ACV_CASE(1) FDLP_ACV_CASE(2) FDLP_ACV_CASE(3) FDLP_ACV_CASE(4) FDLP_ACV_CASE(5) FDLP_ACV_CASE(6)
+    FDLP_ACV_CASE(7) FDLP_ACV_CASE(8) FDLP_ACV_CASE(9) FDLP_ACV_CASE(10) FDLP_ACV_CASE(11) FDLP_ACV_CASE(12)
+    FDLP_ACV_CASE(13) FDLP_ACV_CASE(14) FDLP_ACV_CASE(15) FDLP_ACV_CASE(16) FDLP_ACV_CASE(17) FDLP_ACV_CASE(18)
+    FDLP_ACV_CASE(19) FDLP_ACV_CASE(20) FDLP_ACV_CASE(21) FDLP_ACV_CASE(22) FDLP_ACV_CASE(23) FDLP_ACV_CASE(24)
+    FDLP_ACV_CASE(25) FDLP_ACV_CASE(26) FDLP_ACV_CASE(27) FDLP_ACV_CASE(28) FDLP_ACV_CASE(29) FDLP_ACV_CASE(30)
+#undef FDLP_ACV_CASE
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* dense, int items,
+                           double* r, hipStream_t s) {
+  static const bool use_mfma = getenv("FDLP_AUTOCORR_MFMA") != nullptr;
+  if (!use_mfma && autocorr_valu_lags_per_group(c.nlags) <= 30)
+    return launch_autocorr_valu(c, dct, dense, items, r, s);
+  return launch_autocorr_any(c, dct, dense, items, r, nullptr, nullptr, s);
+}
+
+hipError_t launch_band_fused(const DevConsts& c, int odd_zero, const double* dct, int items, double* r_dbg,
+                             double* env, hipStream_t s) {
+  LpcTail T;
+  T.p = c.p; T.nlags = c.nlags; T.M = c.M; T.Me = c.Me; T.kk = c.kk; T.odd_zero = odd_zero;
+  T.weights = c.weights; T.env_cos = c.env_cos; T.env_nfft = c.env_nfft; T.env_win = c.env_win;
+  return launch_autocorr_any(c, dct, nullptr, items, r_dbg, &T, env, s);
 }
 
 template <int SL>

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -180,6 +181,7 @@ struct fdlp_plan {
   // optional per-stage HIP-event timing (fdlp_set_profiling / fdlp_stage_times)
   bool profiling = false;
   bool debug_intermediates = false;  // keep a/gg/cep of the fused LPC kernel for fdlp_debug_fetch
+  bool fused = false;                // autocorrelation + LPC tail in one kernel (FDLP_FUSE_TAIL=1)
   std::vector<std::vector<hipEvent_t>> prof_pending;
   double prof_ms[FDLP_NUM_STAGES] = {0};
   int prof_calls = 0;
@@ -403,6 +405,8 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   const std::vector<double2> om1 = omega(N1), om2 = omega(N2);
 
   p->max_frames = c.max_frames;
+  // the fused autocorr+LPC-tail kernel measured slower (35.7 vs 25.5+3.9 ms, r01); opt-in only
+  p->fused = fdlp::band_fused_fits(p->nlags, p->p, p->M, p->kk) != 0 && getenv("FDLP_FUSE_TAIL") != nullptr;
   if (device < 0) {  // host-only plan: geometry, filterbank, weights and OLA tables, no compute
     *out = p;
     return FDLP_OK;
@@ -591,11 +595,17 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
   HIP_TRY(mark(1));
   HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z, (int)nf, p->ws.dct, p->d_om2, s));
   HIP_TRY(mark(2));
-  HIP_TRY(fdlp::launch_autocorr(p->dc, p->ws.dct, nullptr, items, p->ws.r, s));
-  HIP_TRY(mark(3));
-  HIP_TRY(fdlp::launch_lpc_env(p->dc, p->cfg.odd_mod_zero, p->ws.r, items, p->ws.env,
-                               p->debug_intermediates ? p->ws.a : nullptr, p->debug_intermediates ? p->ws.gg : nullptr,
-                               p->debug_intermediates ? p->ws.cep : nullptr, s));
+  if (p->fused && !p->debug_intermediates) {
+    // autocorrelation + LPC tail in one launch (stage 3 is then empty)
+    HIP_TRY(fdlp::launch_band_fused(p->dc, p->cfg.odd_mod_zero, p->ws.dct, items, p->ws.r, p->ws.env, s));
+    HIP_TRY(mark(3));
+  } else {
+    HIP_TRY(fdlp::launch_autocorr(p->dc, p->ws.dct, nullptr, items, p->ws.r, s));
+    HIP_TRY(mark(3));
+    HIP_TRY(fdlp::launch_lpc_env(p->dc, p->cfg.odd_mod_zero, p->ws.r, items, p->ws.env,
+                                 p->debug_intermediates ? p->ws.a : nullptr, p->debug_intermediates ? p->ws.gg : nullptr,
+                                 p->debug_intermediates ? p->ws.cep : nullptr, s));
+  }
   HIP_TRY(mark(4));
   HIP_TRY(fdlp::launch_ola_log(p->dc, p->ws.env, p->d_frames, p->d_utts, b->n_utt, maxL, b->out_dev,
                                b->out_f64_dev, b->ark_decimals, s));
