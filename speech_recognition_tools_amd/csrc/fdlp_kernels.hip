@@ -1077,8 +1077,10 @@ hipError_t launch_autocorr_valu(const DevConsts& c, const double* dct, const dou
 
 hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* dense, int items,
                            double* r, hipStream_t s) {
-  static const bool use_mfma = getenv("FDLP_AUTOCORR_MFMA") != nullptr;
-  if (!use_mfma && autocorr_valu_lags_per_group(c.nlags) <= 30)
+  // MFMA is the default: measured 25.1 ms vs 27.1 ms (VALU) per 4096-frame batch on MI355X, the
+  // VALU variant clocks down to ~1.95 GHz under full fp64 FMA load.  FDLP_AUTOCORR_VALU=1 selects it.
+  static const bool use_valu = getenv("FDLP_AUTOCORR_VALU") != nullptr;
+  if (use_valu && autocorr_valu_lags_per_group(c.nlags) <= 30)
     return launch_autocorr_valu(c, dct, dense, items, r, s);
   return launch_autocorr_any(c, dct, dense, items, r, nullptr, nullptr, s);
 }
