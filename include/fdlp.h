@@ -127,6 +127,17 @@ int fdlp_compute(fdlp_plan* plan, const fdlp_batch* batch, void* stream);
 /* Keep the fused LPC kernel's a/gg/cep in the workspace (off by default; needed by
  * fdlp_debug_fetch for those three arrays). */
 int fdlp_set_debug(fdlp_plan* plan, int32_t keep_intermediates);
+/* Autocorrelation algorithm (stage 2).  FDLP_AC_DIRECT: per band, over the taps >= support_eps *
+ * peak.  FDLP_AC_STRUCTURED: exact (no tap truncation) skirt-factorised algorithm for the cochlear
+ * filterbank with a fixed slope (fbank_type cochlear,..,fixed=1,..; DESIGN.md "Structured
+ * autocorrelation").  FDLP_AC_AUTO (plan default) picks STRUCTURED when the filterbank allows it.
+ * fdlp_set_autocorr_path returns FDLP_E_INVALID when STRUCTURED is not available;
+ * fdlp_autocorr_path returns the path in use (DIRECT or STRUCTURED) or a negative error code. */
+#define FDLP_AC_AUTO 0
+#define FDLP_AC_DIRECT 1
+#define FDLP_AC_STRUCTURED 2
+int fdlp_set_autocorr_path(fdlp_plan* plan, int32_t path);
+int fdlp_autocorr_path(const fdlp_plan* plan);
 /* Reads back the intermediates of the most recent fdlp_compute (parity/debug; synchronous):
  * any pointer may be NULL.  Layouts: dct [F,N]; r [F,B,nlags]; a [F,B,order+1]; gg [F,B];
  * cep [F,B,coeff_num]; env [F,B,kk]. */

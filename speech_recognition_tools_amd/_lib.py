@@ -76,6 +76,8 @@ SIGNATURES = {
     "fdlp_debug_fetch": (c_i32, [c_p, c_i32, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl]),
     "fdlp_set_profiling": (c_i32, [c_p, c_i32]),
     "fdlp_set_debug": (c_i32, [c_p, c_i32]),
+    "fdlp_set_autocorr_path": (c_i32, [c_p, c_i32]),
+    "fdlp_autocorr_path": (c_i32, [c_p]),
     "fdlp_stage_times": (c_i32, [c_p, P_dbl, P_i32]),
     "fdlp_dct_rows": (c_i32, [c_p, c_p, c_i32, c_p, c_p]),
     "fdlp_lpc_rows": (c_i32, [c_p, c_p, c_i32, c_p, c_p, c_p, c_p]),

@@ -47,6 +47,12 @@ struct DevConsts {
   const double* env_win;   // [kk, 2] (hanning(kk)[t], hamming(kk)[t]) interleaved (:205)
   const double* tw1;       // [N1 * N2] four-step twiddles exp(-2*pi*i*n2*k1/N) (complex)
   const double* post;      // [N] complex exp(-i*pi*k/(2N)) (Makhoul post-twiddle)
+  // structured autocorrelation (cochlear filterbank, fixed skirt slope); null when not used
+  const double* sk_e;      // [2, N] E = 10^(a (fw - c0)) (lower skirt), E' = 10^(-b (fw - c0)) (upper)
+  const int2* sk_thr;      // [2, B] (S, band) sorted by S descending: S = N - m1_j (lower), m2_j (upper)
+  const double* sk_k;      // [2, B] K_j = 10^(a (w - 2 fc_j + 2 c0)), K'_j = 10^(b (2 fc_j + w - 2 c0))
+  const int2* sk_reg;      // [B] (m1_j, m2_j): lower skirt [0,m1), flat top [m1,m2), upper skirt [m2,N)
+  int sk_min[2];           // smallest threshold per skirt
 };
 
 }  // namespace fdlp
@@ -71,6 +77,8 @@ hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const 
                            int nframes, double* dct, const double2* om2, hipStream_t s);
 hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* dense_rows,
                            int nframes_or_items, double* r, hipStream_t s);
+hipError_t launch_autocorr_structured(const DevConsts& c, const double* dct, int nframes, double* r,
+                                      double* rup, hipStream_t s);
 hipError_t launch_levinson(const DevConsts& c, const double* r, int items, double* a,
                            double* gg, hipStream_t s);
 hipError_t launch_cepstrum(int p, int M, const double* a, const double* gg, int items,

@@ -538,6 +538,291 @@ __global__ __launch_bounds__(64, 4) void autocorr_kernel(DevConsts c, const doub
   }
 }
 
+// -----------------------------------------------------------------------------------------
+// 3s. Structured autocorrelation for the cochlear filterbank with a fixed skirt slope
+//     (createFbankCochlear, features.py:193-219, fixed == 1; DESIGN.md "Structured
+//     autocorrelation").  Band j's taps are 10^(a(d+w/2)) on its lower skirt [0,m1), 1 on the
+//     flat top [m1,m2) and 10^(-b(d-w/2)) on the upper skirt [m2,N), d = fw(m) - fc_j.  Inside
+//     one skirt the product of two taps factorises, W[m] W[m'] = K_j E[m] E[m'], so the pairs of
+//     r_j[l] with both ends on the lower (upper) skirt are K_j (K'_j) times a truncated
+//     autocorrelation of the band-independent signal y = E.D (z = E'.D): ONE sweep per frame and
+//     skirt, with a snapshot at every band's boundary, replaces 80 per-band passes.  The flat-top
+//     pairs and the pairs that straddle a region boundary or the circular wrap are summed per band
+//     with the true taps (ac_band_kernel).  No tap is truncated (support_eps does not apply).
+// -----------------------------------------------------------------------------------------
+
+// Diagonal sums r[L] = sum_i C_{(L+i)>>4}[i][(L+i)&15] of the NT lag tiles for the lags owned by
+// this lane (L = lane + 64 q), through a padded lag-major LDS image, G tiles at a time.
+// ep holds (16 G + 15) * 17 doubles.  Block = one wave.
+template <int NT, int G, int NLPL>
+__device__ __forceinline__ void diag_sums(const dbl4* acc, double* ep, int nlags, int lane, double* mine) {
+#pragma unroll
+  for (int q = 0; q < NLPL; ++q) mine[q] = 0.0;
+  const int col = lane & 15;
+  const int row0 = lane >> 4;
+#pragma unroll
+  for (int tg = 0; tg < NT; tg += G) {
+    const int lag_base = 16 * tg - 15;
+#pragma unroll
+    for (int t = tg; t < tg + G && t < NT; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + 4 * r;
+        ep[(16 * t + col - row - lag_base) * 17 + row] = acc[t][r];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NLPL; ++q) {
+      const int L = lane + 64 * q;
+      if (L < nlags && L >= lag_base && L < 16 * (tg + G)) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int t = (L + i) >> 4;
+          if (t >= tg && t < tg + G && t < NT) s += ep[(L - lag_base) * 17 + i];
+        }
+        mine[q] += s;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// One MFMA k-step of the lag tiles: A = x[P + 16 kk + i] (masked to [lo, hi)), B_t = x[P + 16(kk+t) + jj]
+// read from a window w (w points at the lane's A element; B_t is w[16 t]).
+template <int NT>
+__device__ __forceinline__ void lag_step(dbl4* acc, const double* w, bool keep) {
+  const double a = keep ? w[0] : 0.0;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, w[16 * t], acc[t], 0, 0, 0);
+}
+
+// Skirt sweep: one wave per (frame, skirt).  Skirt 0 walks the reversed lower-skirt signal
+// s[n] = E[N-1-n] D[N-1-n], skirt 1 the upper-skirt signal s[n] = E'[n] D[n] (s = 0 past N, no wrap).
+// Positions are consumed from the top down, 64 per k-step, so after the steps covering [S, N) the
+// tiles hold R(S)[l] = sum_{m >= S} s[m] s[m+l], the autocorrelation of s truncated to [S, N).
+// For skirt 0, S = N - m1_j gives the lower-skirt pairs of band j; for skirt 1, S = m2_j the upper.
+// A threshold inside a k-step splits it into two A-masked steps around the snapshot.
+template <int NT, int G>
+__global__ __launch_bounds__(64, 2) void ac_sweep_kernel(DevConsts c, const double* __restrict__ dct,
+                                                         double* __restrict__ rlow, double* __restrict__ rup) {
+  static_assert(16 * NT <= kAcChunk, "window halo must fit one chunk");
+  constexpr int NLPL = (16 * NT + 63) / 64;
+  constexpr int kEpi = (16 * G + 15) * 17;
+  __shared__ double xs[2 * kAcRing];
+  __shared__ double ep[kEpi];
+
+  const int f = blockIdx.x >> 1;
+  const int sk = blockIdx.x & 1;
+  const int lane = threadIdx.x;
+  const int N = c.N, B = c.B, nlags = c.nlags;
+  const double* drow = dct + (int64_t)f * N;
+  const double* ew = c.sk_e + (int64_t)sk * N;
+  const int2* thr = c.sk_thr + sk * B;
+  const double* ks = c.sk_k + sk * B;
+  double* out = (sk == 0 ? rlow : rup) + (int64_t)f * B * nlags;
+  const int T0 = ((N + kAcChunk - 1) / kAcChunk) * kAcChunk;
+  const int bmin = c.sk_min[sk] >> 6;
+  const int nblk = (T0 >> 6) - bmin;
+  const int nchunks = (nblk + kAcPer - 1) / kAcPer;
+  const int i_lane = lane & 15;
+  const int kk_lane = lane >> 4;
+
+  dbl4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+  double sv[kAcPer];
+  auto fetch = [&](int ch) {  // chunk ch = positions [T0 - 256 (ch+1), T0 - 256 ch)
+#pragma unroll
+    for (int q = 0; q < kAcPer; ++q) {
+      const int n = T0 - kAcChunk * (ch + 1) + 64 * q + lane;
+      double v = 0.0;
+      if (n >= 0 && n < N) {
+        const int m = sk == 0 ? N - 1 - n : n;
+        v = ew[m] * drow[m];
+      }
+      sv[q] = v;
+    }
+  };
+  auto store = [&](int ch) {
+#pragma unroll
+    for (int q = 0; q < kAcPer; ++q) {
+      const int slot = (T0 - kAcChunk * (ch + 1) + 64 * q + lane) & (kAcRing - 1);
+      xs[slot] = sv[q];
+      xs[slot + kAcRing] = sv[q];
+    }
+  };
+  // thresholds are consumed in order; the next one is kept in a register
+  int k = 0;
+  int nextS = B > 0 ? thr[0].x : -1;
+  auto snapshot = [&]() {
+    double mine[NLPL];
+    diag_sums<NT, G, NLPL>(acc, ep, nlags, lane, mine);
+    const int j = thr[k].y;
+    const double K = ks[j];
+#pragma unroll
+    for (int q = 0; q < NLPL; ++q) {
+      const int L = lane + 64 * q;
+      if (L < nlags) out[(int64_t)j * nlags + L] = K * mine[q];
+    }
+    ++k;
+    nextS = k < B ? thr[k].x : -1;
+  };
+  auto step = [&](int P, int lo, int hi) {
+    const int pa = P + 16 * kk_lane + i_lane;
+    lag_step<NT>(acc, xs + (P & (kAcRing - 1)) + 16 * kk_lane + i_lane, pa >= lo && pa < hi);
+  };
+
+#pragma unroll
+  for (int q = 0; q < kAcPer; ++q) {  // chunk -1 (above T0) is zero
+    const int slot = (T0 + 64 * q + lane) & (kAcRing - 1);
+    xs[slot] = 0.0;
+    xs[slot + kAcRing] = 0.0;
+  }
+  fetch(0);
+  store(0);
+  if (nchunks > 1) fetch(1);
+  __syncthreads();
+  for (int ch = 0; ch < nchunks; ++ch) {
+    for (int q = kAcPer - 1; q >= 0; --q) {
+      const int P = T0 - kAcChunk * (ch + 1) + 64 * q;
+      if ((P >> 6) < bmin) break;
+      int hiM = P + 64;
+      while (nextS >= hiM) snapshot();
+      while (nextS > P) {
+        step(P, nextS, hiM);
+        hiM = nextS;
+        snapshot();
+      }
+      step(P, P, hiM);
+    }
+    __syncthreads();
+    if (ch + 1 < nchunks) store(ch + 1);  // into the slots of chunk ch-1
+    if (ch + 2 < nchunks) fetch(ch + 2);
+    __syncthreads();
+  }
+  while (k < B) snapshot();
+}
+
+// Per (frame, band): flat-top pairs (unit taps on [m1, m2)), the pairs straddling m1, m2 and the
+// circular wrap at N (true taps W_j D), plus the two skirt snapshots from ac_sweep_kernel:
+//   r_j[l] = K_j R_y(N-m1_j)[l] + flat + straddles + K'_j R_z(m2_j)[l]
+// r holds the lower-skirt term on entry and r_j on exit.
+template <int NT>
+__global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const double* __restrict__ dct,
+                                                        double* __restrict__ r, const double* __restrict__ rup) {
+  static_assert(16 * NT <= kAcChunk, "window halo must fit one chunk");
+  constexpr int G = 2;
+  constexpr int NLPL = (16 * NT + 63) / 64;
+  constexpr int kEpi = (16 * G + 15) * 17;
+  constexpr int kWin = (16 * NT + 63) / 64 * 64;         // A window of a straddle (>= nlags - 1)
+  constexpr int kLds = 2 * kAcRing;
+  static_assert(kEpi <= kLds && 2 * kWin + 16 * NT <= kLds, "LDS regions");
+  __shared__ double xs[kLds];
+
+  const int item = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int N = c.N, nlags = c.nlags;
+  const int f = item / c.B, j = item % c.B;
+  const int2 reg = c.sk_reg[j];
+  const int m1 = reg.x, m2 = reg.y;
+  const double* drow = dct + (int64_t)f * N;
+  const double* wrow = c.fbank + (int64_t)j * N;
+  const int i_lane = lane & 15;
+  const int kk_lane = lane >> 4;
+
+  dbl4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+  // flat top: x = D on [m1, m2), 0 elsewhere
+  {
+    const int lo = m1, hi = m2;
+    const int nsteps = (hi - lo + 63) / 64;
+    const int nchunks = (nsteps + kAcPer - 1) / kAcPer;
+    double dv[kAcPer];
+    auto fetch = [&](int ch) {
+#pragma unroll
+      for (int q = 0; q < kAcPer; ++q) {
+        const int pos = lo + kAcChunk * ch + 64 * q + lane;
+        dv[q] = pos < hi ? drow[pos] : 0.0;
+      }
+    };
+    auto store = [&](int ch) {
+#pragma unroll
+      for (int q = 0; q < kAcPer; ++q) {
+        const int slot = (kAcChunk * ch + 64 * q + lane) & (kAcRing - 1);
+        xs[slot] = dv[q];
+        xs[slot + kAcRing] = dv[q];
+      }
+    };
+    if (nsteps > 0) {
+      fetch(0);
+      store(0);
+      fetch(1);
+      store(1);
+      fetch(2);
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ++ch) {
+      const int s_end = min(kAcPer, nsteps - kAcPer * ch);
+      const int rbase = (kAcChunk * ch) & (kAcRing - 1);
+      for (int st = 0; st < s_end; ++st)
+        lag_step<NT>(acc, xs + rbase + 64 * st + 16 * kk_lane + i_lane, true);
+      __syncthreads();
+      store(ch + 2);
+      if (ch + 3 <= nchunks) fetch(ch + 3);
+      __syncthreads();
+    }
+  }
+
+  // straddles: A = x[m], m in [lb, b) (the region just below boundary b, at most nlags-1 long),
+  // B = x[(m + l) mod N] for m + l >= b, x = W_j D
+  double* xa = xs;
+  double* xb = xs + kWin;
+#pragma unroll 1
+  for (int e = 0; e < 3; ++e) {
+    const int b = e == 0 ? m1 : (e == 1 ? m2 : N);
+    int lb = e == 0 ? 0 : (e == 1 ? m1 : m2);
+    lb = max(lb, b - (nlags - 1));
+    if (lb >= b) continue;
+    __syncthreads();
+    for (int q = lane; q < kWin + 16 * NT; q += 64) {  // B reads reach xb[kWin - 1 + 16 NT - 1]
+      const int pos = b - kWin + q;
+      double x = 0.0;
+      if (pos >= lb) {
+        const int pm = pos >= N ? pos - N : pos;
+        x = wrow[pm] * drow[pm];
+      }
+      xb[q] = pos >= b ? x : 0.0;
+      if (q < kWin) xa[q] = pos < b ? x : 0.0;
+    }
+    __syncthreads();
+    for (int st = (lb - b + kWin) >> 6; st < kWin / 64; ++st) {
+      const int w = 64 * st + 16 * kk_lane + i_lane;
+      const double a = xa[w];
+      // tile t reads B positions up to b - kWin + 64 st + 63 + 16 t; below b they are all zero
+      const int tmin = (kWin - 64 * st - 48) >> 4;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (t >= tmin) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, xb[w + 16 * t], acc[t], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  double mine[NLPL];
+  diag_sums<NT, G, NLPL>(acc, xs, nlags, lane, mine);
+#pragma unroll
+  for (int q = 0; q < NLPL; ++q) {
+    const int L = lane + 64 * q;
+    if (L < nlags) {
+      const int64_t o = (int64_t)item * nlags + L;
+      r[o] = mine[q] + r[o] + rup[o];
+    }
+  }
+}
+
 template <int NT>
 constexpr int autocorr_lds_doubles() {
   constexpr int kEpi = (16 * 4 + 15) * 17;
@@ -1083,6 +1368,33 @@ hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* 
   if (use_valu && autocorr_valu_lags_per_group(c.nlags) <= 30)
     return launch_autocorr_valu(c, dct, dense, items, r, s);
   return launch_autocorr_any(c, dct, dense, items, r, nullptr, nullptr, s);
+}
+
+template <int NT>
+static hipError_t launch_struct_nt(const DevConsts& c, const double* dct, int nframes, double* r, double* rup,
+                                   hipStream_t s) {
+  static const bool full = getenv("FDLP_SWEEP_FULL_EPI") != nullptr;
+  if (full)
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, NT>), dim3(2 * nframes), dim3(64), 0, s, c, dct, r, rup);
+  else
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, 4>), dim3(2 * nframes), dim3(64), 0, s, c, dct, r, rup);
+  hipLaunchKernelGGL(ac_band_kernel<NT>, dim3(nframes * c.B), dim3(64), 0, s, c, dct, r, rup);
+  return hipGetLastError();
+}
+
+hipError_t launch_autocorr_structured(const DevConsts& c, const double* dct, int nframes, double* r,
+                                      double* rup, hipStream_t s) {
+  if (nframes <= 0) return hipSuccess;
+  if (!c.sk_e || !c.sk_thr || !c.sk_k || !c.sk_reg) return hipErrorInvalidValue;
+  switch (autocorr_tiles(c.nlags)) {
+#define FDLP_ST_CASE(n) case n: return launch_struct_nt<n>(c, dct, nframes, r, rup, s);
+    FDLP_ST_CASE(1) FDLP_ST_CASE(2) FDLP_ST_CASE(3) FDLP_ST_CASE(4) FDLP_ST_CASE(5)
+    FDLP_ST_CASE(6) FDLP_ST_CASE(7) FDLP_ST_CASE(8) FDLP_ST_CASE(9) FDLP_ST_CASE(10)
+    FDLP_ST_CASE(11) FDLP_ST_CASE(12) FDLP_ST_CASE(13) FDLP_ST_CASE(14) FDLP_ST_CASE(15)
+    FDLP_ST_CASE(16)
+#undef FDLP_ST_CASE
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_band_fused(const DevConsts& c, int odd_zero, const double* dct, int items, double* r_dbg,

@@ -103,6 +103,71 @@ std::vector<double> fbank_mel(int nf, int nfft, int srate, double wf, int* ncol_
   return W;
 }
 
+// Structured-autocorrelation tables (DESIGN.md "Structured autocorrelation") for
+// createFbankCochlear with fixed == 1: every band's taps must follow the lower-skirt / flat-top /
+// upper-skirt pattern along m (classified exactly like fbank_cochlear), and the skirt factors
+// E, E', K, K' must stay well inside the fp64 range.  Returns false otherwise (direct path).
+struct SkirtTables {
+  std::vector<double> e;    // [2, N]
+  std::vector<int2> thr;    // [2, B]
+  std::vector<double> k;    // [2, B]
+  std::vector<int2> reg;    // [B]
+  int smin[2] = {0, 0};
+};
+
+bool skirt_tables(const fdlp_config& c, int B, int N, int nfft, SkirtTables* T) {
+  if (c.fbank_kind != FDLP_FBANK_COCHLEAR || c.fixed != 1) return false;
+  const double wf = c.warp_fact, om = c.om_w, a = c.alp, b = c.bet;
+  if (!std::isfinite(wf) || !std::isfinite(om) || !std::isfinite(a) || !std::isfinite(b)) return false;
+  auto bark = [wf](double x) { return 6.0 * asinh((x / wf) / 600.0); };
+  const double fmax = (double)c.srate / 2.0;
+  const std::vector<double> cf = linspace(0.0, bark(fmax), B);
+  const int ncol = (int)floor((double)nfft / 2.0 + 1.0);
+  if (ncol - 1 != N) return false;
+  std::vector<double> fl = linspace(0.0, fmax, ncol);
+  for (auto& v : fl) v = bark(v);
+  T->reg.resize(B);
+  for (int j = 0; j < B; ++j) {
+    int state = 0, m1 = 0, m2 = 0;
+    for (int m = 0; m < N; ++m) {
+      const double d = fl[m] - cf[j];
+      const int cls = d <= -om / 2.0 ? 0 : ((d > -om / 2.0 && d < om / 2.0) ? 1 : 2);
+      if (cls < state) return false;
+      state = cls;
+      if (cls == 0) m1 = m + 1;
+      if (cls <= 1) m2 = m + 1;
+    }
+    if (m2 < m1) m2 = m1;
+    T->reg[j] = make_int2(m1, m2);
+  }
+  const long double c0 = 0.5L * ((long double)fl[0] + (long double)fl[N - 1]);
+  const long double span = std::max(fabsl((long double)fl[N - 1] - c0), fabsl((long double)fl[0] - c0));
+  if (fabsl((long double)a) * span > 60.0L || fabsl((long double)b) * span > 60.0L) return false;
+  T->e.resize(2 * (size_t)N);
+  for (int m = 0; m < N; ++m) {
+    const long double x = (long double)fl[m] - c0;
+    T->e[m] = (double)powl(10.0L, (long double)a * x);
+    T->e[(size_t)N + m] = (double)powl(10.0L, -(long double)b * x);
+  }
+  T->k.resize(2 * (size_t)B);
+  for (int j = 0; j < B; ++j) {
+    const long double ea = (long double)a * ((long double)om - 2.0L * cf[j] + 2.0L * c0);
+    const long double eb = (long double)b * (2.0L * cf[j] + (long double)om - 2.0L * c0);
+    if (fabsl(ea) > 150.0L || fabsl(eb) > 150.0L) return false;
+    T->k[j] = (double)powl(10.0L, ea);
+    T->k[(size_t)B + j] = (double)powl(10.0L, eb);
+  }
+  T->thr.resize(2 * (size_t)B);
+  for (int sk = 0; sk < 2; ++sk) {
+    std::vector<int2> t(B);
+    for (int j = 0; j < B; ++j) t[j] = make_int2(sk == 0 ? N - T->reg[j].x : T->reg[j].y, j);
+    std::stable_sort(t.begin(), t.end(), [](const int2& u, const int2& v) { return u.x > v.x; });
+    for (int j = 0; j < B; ++j) T->thr[(size_t)sk * B + j] = t[j];
+    T->smin[sk] = t[B - 1].x;
+  }
+  return true;
+}
+
 // radix split of n over the supported radices (4s first, then 2, 3, 5, 7)
 bool factor_radices(int n, fdlp::DftPlan* d) {
   d->n = n;
@@ -182,6 +247,11 @@ struct fdlp_plan {
   bool profiling = false;
   bool debug_intermediates = false;  // keep a/gg/cep of the fused LPC kernel for fdlp_debug_fetch
   bool fused = false;                // autocorrelation + LPC tail in one kernel (FDLP_FUSE_TAIL=1)
+  bool sk_avail = false;             // structured autocorrelation possible for this filterbank
+  int ac_path = FDLP_AC_DIRECT;      // FDLP_AC_DIRECT or FDLP_AC_STRUCTURED
+  SkirtTables sk;
+  double *d_sk_e = nullptr, *d_sk_k = nullptr, *r_up = nullptr;
+  int2 *d_sk_thr = nullptr, *d_sk_reg = nullptr;
   std::vector<std::vector<hipEvent_t>> prof_pending;
   double prof_ms[FDLP_NUM_STAGES] = {0};
   int prof_calls = 0;
@@ -210,7 +280,8 @@ int free_plan(fdlp_plan* p) {
     for (auto e : ev) (void)hipEventDestroy(e);
   void* devs[] = {p->d_fbank, p->d_hamming, p->d_weights, p->d_env_cos, p->d_env_win, p->d_tw1, p->d_post,
                   p->d_om1, p->d_om2, p->d_lo, p->d_hi, p->ws.z, p->ws.dct, p->ws.r, p->ws.a, p->ws.gg,
-                  p->ws.cep, p->ws.env, p->d_frames, p->d_utts};
+                  p->ws.cep, p->ws.env, p->d_frames, p->d_utts, p->d_sk_e, p->d_sk_k, p->r_up,
+                  p->d_sk_thr, p->d_sk_reg};
   for (void* d : devs)
     if (d) (void)hipFree(d);
   if (p->h_frames) (void)hipHostFree(p->h_frames);
@@ -353,6 +424,9 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
     p->hi[j] = hi;
   }
 
+  p->sk_avail = skirt_tables(c, p->B, p->N, p->nfft, &p->sk);
+  p->ac_path = p->sk_avail && getenv("FDLP_AUTOCORR_DIRECT") == nullptr ? FDLP_AC_STRUCTURED : FDLP_AC_DIRECT;
+
   // modulation weights (:94-118)
   const int M = p->M;
   p->weights_host.assign((size_t)3 * M, 1.0);
@@ -432,6 +506,14 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   d.kk = p->kk; d.env_nfft = p->env_nfft;
   d.fbank = p->d_fbank; d.lo = p->d_lo; d.hi = p->d_hi; d.hamming = p->d_hamming; d.weights = p->d_weights;
   d.env_cos = p->d_env_cos; d.env_win = p->d_env_win; d.tw1 = p->d_tw1; d.post = p->d_post;
+  if (p->sk_avail) {
+    PLAN_TRY(upload(&p->d_sk_e, p->sk.e.data(), p->sk.e.size()));
+    PLAN_TRY(upload(&p->d_sk_k, p->sk.k.data(), p->sk.k.size()));
+    PLAN_TRY(upload(&p->d_sk_thr, p->sk.thr.data(), p->sk.thr.size()));
+    PLAN_TRY(upload(&p->d_sk_reg, p->sk.reg.data(), p->sk.reg.size()));
+    d.sk_e = p->d_sk_e; d.sk_k = p->d_sk_k; d.sk_thr = p->d_sk_thr; d.sk_reg = p->d_sk_reg;
+    d.sk_min[0] = p->sk.smin[0]; d.sk_min[1] = p->sk.smin[1];
+  }
 
   // workspace
   const size_t F = (size_t)c.max_frames, items = F * p->B;
@@ -443,6 +525,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
       hipMalloc((void**)&p->ws.gg, sizeof(double) * items) != hipSuccess ||
       hipMalloc((void**)&p->ws.cep, sizeof(double) * items * M) != hipSuccess ||
       hipMalloc((void**)&p->ws.env, sizeof(double) * items * p->kk) != hipSuccess ||
+      (p->sk_avail && hipMalloc((void**)&p->r_up, sizeof(double) * items * p->nlags) != hipSuccess) ||
       hipMalloc((void**)&p->d_frames, sizeof(fdlp::FrameDesc) * F) != hipSuccess ||
       hipMalloc((void**)&p->d_utts, sizeof(fdlp::UttDesc) * F) != hipSuccess ||
       hipHostMalloc((void**)&p->h_frames, sizeof(fdlp::FrameDesc) * F, hipHostMallocDefault) != hipSuccess ||
@@ -595,7 +678,13 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
   HIP_TRY(mark(1));
   HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z, (int)nf, p->ws.dct, p->d_om2, s));
   HIP_TRY(mark(2));
-  if (p->fused && !p->debug_intermediates) {
+  if (p->ac_path == FDLP_AC_STRUCTURED) {
+    HIP_TRY(fdlp::launch_autocorr_structured(p->dc, p->ws.dct, (int)nf, p->ws.r, p->r_up, s));
+    HIP_TRY(mark(3));
+    HIP_TRY(fdlp::launch_lpc_env(p->dc, p->cfg.odd_mod_zero, p->ws.r, items, p->ws.env,
+                                 p->debug_intermediates ? p->ws.a : nullptr, p->debug_intermediates ? p->ws.gg : nullptr,
+                                 p->debug_intermediates ? p->ws.cep : nullptr, s));
+  } else if (p->fused && !p->debug_intermediates) {
     // autocorrelation + LPC tail in one launch (stage 3 is then empty)
     HIP_TRY(fdlp::launch_band_fused(p->dc, p->cfg.odd_mod_zero, p->ws.dct, items, p->ws.r, p->ws.env, s));
     HIP_TRY(mark(3));
@@ -612,6 +701,27 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
   HIP_TRY(mark(5));
   if (p->profiling) p->prof_pending.push_back(ev);
   return FDLP_OK;
+}
+
+int fdlp_set_autocorr_path(fdlp_plan* p, int32_t path) {
+  if (!p) return fail(FDLP_E_INVALID, "fdlp_set_autocorr_path: null plan");
+  if (path == FDLP_AC_AUTO) {
+    p->ac_path = p->sk_avail ? FDLP_AC_STRUCTURED : FDLP_AC_DIRECT;
+  } else if (path == FDLP_AC_DIRECT) {
+    p->ac_path = FDLP_AC_DIRECT;
+  } else if (path == FDLP_AC_STRUCTURED) {
+    if (!p->sk_avail)
+      return fail(FDLP_E_INVALID, "structured autocorrelation needs the cochlear filterbank with fixed=1");
+    p->ac_path = FDLP_AC_STRUCTURED;
+  } else {
+    return fail(FDLP_E_INVALID, "fdlp_set_autocorr_path: unknown path");
+  }
+  return FDLP_OK;
+}
+
+int fdlp_autocorr_path(const fdlp_plan* p) {
+  if (!p) return fail(FDLP_E_INVALID, "fdlp_autocorr_path: null plan");
+  return p->ac_path;
 }
 
 int fdlp_set_debug(fdlp_plan* p, int32_t keep_intermediates) {

@@ -221,6 +221,19 @@ class FdlpPlan:
         check(lib.fdlp_compute(self._h, ctypes.byref(b), ctypes.c_void_p(s.cuda_stream)))
         return out[:total], rows, out64
 
+    AUTOCORR_PATHS = {"auto": 0, "direct": 1, "structured": 2}
+
+    @property
+    def autocorr_path(self) -> str:
+        """'direct' (per band over the taps >= support_eps*peak) or 'structured' (exact
+        skirt-factorised algorithm, cochlear filterbank with fixed=1)."""
+        v = lib.fdlp_autocorr_path(self._h)
+        check(v if v < 0 else 0)
+        return {1: "direct", 2: "structured"}[v]
+
+    def set_autocorr_path(self, path: str = "auto"):
+        check(lib.fdlp_set_autocorr_path(self._h, self.AUTOCORR_PATHS[path]))
+
     def set_debug(self, keep_intermediates: bool = True):
         check(lib.fdlp_set_debug(self._h, int(bool(keep_intermediates))))
 

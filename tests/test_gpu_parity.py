@@ -42,10 +42,11 @@ def _batch_inputs(meta, sig, z):
     return pcm, kw
 
 
-def run_gpu(meta, sig, z, support_eps=None, max_frames=256, debug=False):
+def run_gpu(meta, sig, z, support_eps=None, max_frames=256, debug=False, path="auto"):
     from speech_recognition_tools_amd import FdlpPlan, PyRandom
     cfg = feature_cfg(meta, support_eps)
     plan = FdlpPlan(cfg, device=0, max_frames=max_frames)
+    plan.set_autocorr_path(path)
     if debug:
         plan.set_debug(True)
     utts = meta["utts"]
@@ -60,10 +61,11 @@ def run_gpu(meta, sig, z, support_eps=None, max_frames=256, debug=False):
     return plan, res
 
 
+@pytest.mark.parametrize("path", ["auto", "direct"])
 @pytest.mark.parametrize("name", GOLDEN_SETS)
-def test_pipeline_vs_reference_golden(name):
+def test_pipeline_vs_reference_golden(name, path):
     meta, sig, ref, z = load_golden(name)
-    _, res = run_gpu(meta, sig, z)
+    _, res = run_gpu(meta, sig, z, path=path)
     for u in meta["utts"]:
         f64, f32 = res[u]
         assert f64.shape == ref[u].shape, u
@@ -76,7 +78,7 @@ def test_pipeline_vs_reference_golden(name):
 @pytest.mark.parametrize("eps", [0.0, 1e-20, 1e-16])
 def test_support_eps_variants(eps):
     meta, sig, ref, z = load_golden("wsj")
-    _, res = run_gpu(meta, sig, z, support_eps=eps)
+    _, res = run_gpu(meta, sig, z, support_eps=eps, path="direct")
     for u in meta["utts"]:
         assert np.abs(res[u][0] - ref[u]).max() <= TOL_UTT.get(u, TOL), (eps, u)
 
@@ -121,12 +123,13 @@ def test_stage_dct_and_lpc_vs_reference_stages():
             np.testing.assert_allclose(c[i], z["%s_c%d" % (tag, lim)], rtol=1e-9, atol=1e-9)
 
 
-def test_intermediates_vs_oracle():
+@pytest.mark.parametrize("path", ["structured", "direct"])
+def test_intermediates_vs_oracle(path):
     """Every stage of one utterance against the oracle's intermediates."""
     from oracle import fdlp_oracle as O
     meta, sig, ref, z = load_golden("wsj")
     sub = {"s4p0": sig["s4p0"]}
-    plan, res = run_gpu(dict(meta, utts=["s4p0"]), sub, z, debug=True)
+    plan, res = run_gpu(dict(meta, utts=["s4p0"]), sub, z, debug=True, path=path)
     d = plan.debug_fetch(4)
     keep = O.Intermediates()
     O.FdlpOracle(oracle_cfg(meta)).band_envelopes(sig["s4p0"], keep)
@@ -135,3 +138,43 @@ def test_intermediates_vs_oracle():
     assert rel.max() <= 1e-12
     assert np.abs(d["cep"] - keep.cep).max() <= 1e-5
     assert np.abs(np.log(d["env"][..., 1:-1]) - np.log(keep.env[..., 1:-1])).max() <= 1e-5
+
+
+STRUCT_CFGS = [
+    # (fbank_type, nfilters, fduration, order, coeff_num)
+    ("cochlear,1,1,1,2.5,1", 80, 1.5, 150, 100),     # WSJ / REVERB / CHiME-4 recipes
+    ("cochlear,0.5,2.5,1,1.5,1", 40, 1.0, 60, 60),   # narrow flat top, steep lower skirt
+    ("cochlear,2,0.5,1,4,1.2", 20, 0.5, 30, 40),     # wide flat top, warped axis, short frames
+    ("cochlear,1,1,1,2.5,1", 7, 1.5, 238, 100),      # few wide bands, the largest order
+]
+
+
+@pytest.mark.parametrize("fb,nf,fd,order,cn", STRUCT_CFGS)
+def test_structured_autocorr_matches_oracle(fb, nf, fd, order, cn):
+    """The skirt-factorised autocorrelation equals the oracle's FFT autocorrelation of every band
+    (features.py:223-226) to fp64 rounding, on speech-like and on white input, with the edge bands
+    whose lower skirt (band 0) or upper skirt (last band) is empty."""
+    from oracle import fdlp_oracle as O
+    from speech_recognition_tools_amd import FdlpPlan, FeatureConfig, PyRandom
+    cfg = FeatureConfig(fbank_type=fb, nfilters=nf, fduration=fd, order=order, coeff_num=cn,
+                        coeff_range="0,%d" % cn)
+    plan = FdlpPlan(cfg, device=0, max_frames=64)
+    assert plan.autocorr_path == "structured"
+    plan.set_debug(True)
+    rng = np.random.default_rng(nf + order)
+    T = 16000 + 123
+    t = np.arange(T) / 16000.0
+    speechy = (3000 * np.sin(2 * np.pi * 180 * t) * (1 + np.sin(2 * np.pi * 3 * t))
+               + 200 * rng.standard_normal(T)).astype(np.int16)
+    white = (rng.standard_normal(T) * 8000).astype(np.int16)
+    ocfg = O.FdlpConfig(fbank_type=fb, nfilters=nf, fduration=fd, order=order, coeff_num=cn,
+                        coeff_range="0,%d" % cn)
+    for x in (speechy, white):
+        F, _ = plan.geometry(T)
+        plan.compute(torch.from_numpy(x).cuda(), [T], PyRandom(0).randbits2(F - 1))
+        torch.cuda.synchronize()
+        d = plan.debug_fetch(F)
+        keep = O.Intermediates()
+        O.FdlpOracle(ocfg).band_envelopes(x, keep)
+        rel = np.abs(d["r"] - keep.r).max(axis=-1) / np.abs(keep.r[..., 0])
+        assert rel.max() <= 1e-12, rel.max()

@@ -239,3 +239,19 @@ def test_cli_argparse_surface_matches_reference():
     args = build_parser().parse_args(["a.scp", "out", "--fbank_type=cochlear,1,1,1,2.5,1", "--nfilters=80",
                                       "--coeff_range=0,100", "--order=150", "--add_noise=clean"])
     assert args.nfilters == 80 and args.fbank_type.startswith("cochlear") and args.order == 150
+
+
+def test_autocorr_path_selection():
+    from speech_recognition_tools_amd import FdlpError, FeatureConfig
+    p = _host_plan(FeatureConfig.wsj())
+    assert p.autocorr_path == "structured"
+    p.set_autocorr_path("direct")
+    assert p.autocorr_path == "direct"
+    p.set_autocorr_path("auto")
+    assert p.autocorr_path == "structured"
+    for cfg in (FeatureConfig(), FeatureConfig(fbank_type="cochlear,1,1,0,2.5,1"),   # mel; alpha not fixed
+                FeatureConfig(fbank_type="cochlear,1,9,1,2.5,1")):                    # skirt exponents too wide
+        q = _host_plan(cfg)
+        assert q.autocorr_path == "direct"
+        with pytest.raises(FdlpError, match="structured"):
+            q.set_autocorr_path("structured")
