@@ -68,6 +68,28 @@ def cpu_baseline(cfg_name, T, workers, per_worker):
                        (workers * per_worker, T / 16000.0, per_worker))
 
 
+AC_KERNELS = {"structured": "autocorr stage: ac_sweep_kernel + ac_band_kernel (v_mfma_f64_16x16x4f64)",
+              "direct": "autocorr stage: autocorr_kernel (v_mfma_f64_16x16x4f64)"}
+
+
+def autocorr_flops(plan, support):
+    """Useful fp64 FLOPs of the autocorrelation stage per analysis frame (2 per MAC).
+    direct: nlags MACs per tap of every band support (circular).  structured: the two skirt sweeps,
+    the flat tops and the boundary straddles (DESIGN.md "Structured autocorrelation")."""
+    nl, N = plan.nlags, plan.N
+    lags = np.arange(nl)
+    trunc = lambda n: float(np.maximum(n - lags, 0).sum())      # truncated autocorrelation
+    if plan.autocorr_path != "structured":
+        return 2.0 * nl * float(support.sum())
+    m1, m2 = plan.regions()
+    macs = trunc(int(m1.max())) + trunc(N - int(m2.min()))
+    for j in range(plan.B):
+        macs += trunc(int(m2[j] - m1[j]))
+        for b, lb in ((m1[j], 0), (m2[j], m1[j]), (N, m2[j])):
+            macs += float(np.minimum(lags, min(int(b - lb), nl - 1)).sum())
+    return 2.0 * macs
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -80,6 +102,7 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--cpu-per-worker", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=None, help="sub-batches over two streams (plan default 2)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -109,6 +132,8 @@ def main():
     F_u, L_u = probe.geometry(T)
     frames = F_u * args.utts
     plan = FdlpPlan(cfg, device=local, max_frames=frames)
+    if args.pipeline is not None:
+        plan.set_pipeline(args.pipeline)
     _, lo, hi = probe.fbank()
     support = (hi - lo).astype(np.int64)
 
@@ -144,9 +169,8 @@ def main():
 
     audio_h = world * args.steps * args.utts * T / 16000.0 / 3600.0
     value = audio_h / elapsed
-    # dominant kernel: the MFMA autocorrelation.  Algorithmic FLOPs = 2 * nlags * (taps in the
-    # band supports) per analysis frame (useful MACs only; DESIGN.md "Roofline").
-    flops_per_launch = 2.0 * plan.nlags * float(support.sum()) * frames
+    # dominant stage: the MFMA autocorrelation (DESIGN.md "Roofline": useful MACs only)
+    flops_per_launch = autocorr_flops(plan, support) * frames
     ac_ms = stages["autocorr"] / max(ncalls, 1)
     achieved = flops_per_launch / (ac_ms * 1e-3) / 1e12
     res = {
@@ -166,8 +190,9 @@ def main():
                    "utts_per_step_per_gpu": args.utts, "utt_seconds": args.seconds,
                    "frames_per_step_per_gpu": frames, "nfilters": cfg.nfilters, "order": cfg.order,
                    "coeff_num": cfg.coeff_num, "fbank": cfg.fbank_type, "support_eps": cfg.support_eps,
+                   "autocorr_path": plan.autocorr_path,
                    "parallelism": "scp-shard x%d (no collective)" % world},
-        "roofline": {"bound": "mfma", "kernel": "autocorr_kernel (v_mfma_f64_16x16x4f64)",
+        "roofline": {"bound": "mfma", "kernel": AC_KERNELS[plan.autocorr_path],
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
                      "avg_launch_ms": ac_ms, "algorithmic_flops_per_launch": flops_per_launch},

@@ -138,15 +138,25 @@ int fdlp_set_debug(fdlp_plan* plan, int32_t keep_intermediates);
 #define FDLP_AC_STRUCTURED 2
 int fdlp_set_autocorr_path(fdlp_plan* plan, int32_t path);
 int fdlp_autocorr_path(const fdlp_plan* plan);
+/* Lower-skirt / flat-top / upper-skirt split of every band, [0,m1) [m1,m2) [m2,N), used by the
+ * STRUCTURED path; FDLP_E_INVALID when the filterbank does not have it. */
+int fdlp_plan_regions(const fdlp_plan* plan, int32_t* m1, int32_t* m2);
+/* fdlp_compute splits a batch of F frames into min(n_sub, F/256) sub-batches that alternate
+ * between the caller's stream and a second stream of the plan, so the MFMA-bound autocorrelation
+ * of one sub-batch can overlap the VALU-bound kernels of the other (default 1 = serial: on MI355X
+ * the fp64 MFMA and fp64 VALU work measured no net overlap). */
+int fdlp_set_pipeline(fdlp_plan* plan, int32_t n_sub);
 /* Reads back the intermediates of the most recent fdlp_compute (parity/debug; synchronous):
  * any pointer may be NULL.  Layouts: dct [F,N]; r [F,B,nlags]; a [F,B,order+1]; gg [F,B];
  * cep [F,B,coeff_num]; env [F,B,kk]. */
 int fdlp_debug_fetch(fdlp_plan* plan, int32_t n_frames, double* dct, double* r, double* a,
                      double* gg, double* cep, double* env);
 
-/* Per-stage device time (HIP events on the compute stream) of every fdlp_compute since profiling
- * was (re)enabled.  Stages: 0 frames+column DFT, 1 row DFT+DCT, 2 autocorrelation,
- * 3 fused Levinson+cepstrum+envelope, 4 OLA+log.  fdlp_stage_times synchronises on the events. */
+/* Per-stage device time (HIP events on the stream each stage runs on) of every fdlp_compute since
+ * profiling was (re)enabled.  Stages: 0 frames+column DFT, 1 row DFT+DCT, 2 autocorrelation,
+ * 3 fused Levinson+cepstrum+envelope, 4 OLA+log.  With sub-batch pipelining the stage times are
+ * summed over the sub-batches and overlap each other in wall time.  fdlp_stage_times
+ * synchronises on the events. */
 #define FDLP_NUM_STAGES 5
 int fdlp_set_profiling(fdlp_plan* plan, int32_t enable);
 int fdlp_stage_times(fdlp_plan* plan, double* ms_sum /* [FDLP_NUM_STAGES] */, int32_t* n_calls);

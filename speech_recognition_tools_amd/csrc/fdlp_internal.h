@@ -35,6 +35,14 @@ struct UttDesc {
   int32_t pad;
 };
 
+// One snapshot of a skirt sweep: after the positions >= S are consumed, band `band` receives
+// K times the truncated autocorrelation (structured autocorrelation, fdlp_kernels.hip 3s).
+struct SkSnap {
+  int32_t S;
+  int32_t band;
+  double K;
+};
+
 // Device-resident constants of a plan.
 struct DevConsts {
   int B, N, hop, ext, p, nlags, M, Me, kk, env_nfft;
@@ -49,8 +57,8 @@ struct DevConsts {
   const double* post;      // [N] complex exp(-i*pi*k/(2N)) (Makhoul post-twiddle)
   // structured autocorrelation (cochlear filterbank, fixed skirt slope); null when not used
   const double* sk_e;      // [2, N] E = 10^(a (fw - c0)) (lower skirt), E' = 10^(-b (fw - c0)) (upper)
-  const int2* sk_thr;      // [2, B] (S, band) sorted by S descending: S = N - m1_j (lower), m2_j (upper)
-  const double* sk_k;      // [2, B] K_j = 10^(a (w - 2 fc_j + 2 c0)), K'_j = 10^(b (2 fc_j + w - 2 c0))
+  const SkSnap* sk_snap;   // [2, B] sorted by S descending: S = N - m1_j (lower) / m2_j (upper) with
+                           // K_j = 10^(a (w - 2 fc_j + 2 c0)) / K'_j = 10^(b (2 fc_j + w - 2 c0))
   const int2* sk_reg;      // [B] (m1_j, m2_j): lower skirt [0,m1), flat top [m1,m2), upper skirt [m2,N)
   int sk_min[2];           // smallest threshold per skirt
 };

@@ -604,7 +604,7 @@ __device__ __forceinline__ void lag_step(dbl4* acc, const double* w, bool keep) 
 // tiles hold R(S)[l] = sum_{m >= S} s[m] s[m+l], the autocorrelation of s truncated to [S, N).
 // For skirt 0, S = N - m1_j gives the lower-skirt pairs of band j; for skirt 1, S = m2_j the upper.
 // A threshold inside a k-step splits it into two A-masked steps around the snapshot.
-template <int NT, int G>
+template <int NT, int G, bool SNAP = true>
 __global__ __launch_bounds__(64, 2) void ac_sweep_kernel(DevConsts c, const double* __restrict__ dct,
                                                          double* __restrict__ rlow, double* __restrict__ rup) {
   static_assert(16 * NT <= kAcChunk, "window halo must fit one chunk");
@@ -619,8 +619,7 @@ __global__ __launch_bounds__(64, 2) void ac_sweep_kernel(DevConsts c, const doub
   const int N = c.N, B = c.B, nlags = c.nlags;
   const double* drow = dct + (int64_t)f * N;
   const double* ew = c.sk_e + (int64_t)sk * N;
-  const int2* thr = c.sk_thr + sk * B;
-  const double* ks = c.sk_k + sk * B;
+  const SkSnap* snaps = c.sk_snap + sk * B;
   double* out = (sk == 0 ? rlow : rup) + (int64_t)f * B * nlags;
   const int T0 = ((N + kAcChunk - 1) / kAcChunk) * kAcChunk;
   const int bmin = c.sk_min[sk] >> 6;
@@ -633,42 +632,52 @@ __global__ __launch_bounds__(64, 2) void ac_sweep_kernel(DevConsts c, const doub
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
 
-  double sv[kAcPer];
-  auto fetch = [&](int ch) {  // chunk ch = positions [T0 - 256 (ch+1), T0 - 256 ch)
+  // chunk ch = positions [T0 - 256 (ch+1), T0 - 256 ch); the loads land in registers and are
+  // multiplied only when stored, one chunk later, so their latency hides behind 44 MFMAs
+  double dv[kAcPer], ev[kAcPer];
+  auto fetch = [&](int ch) {
 #pragma unroll
     for (int q = 0; q < kAcPer; ++q) {
       const int n = T0 - kAcChunk * (ch + 1) + 64 * q + lane;
-      double v = 0.0;
-      if (n >= 0 && n < N) {
-        const int m = sk == 0 ? N - 1 - n : n;
-        v = ew[m] * drow[m];
-      }
-      sv[q] = v;
+      const bool ok = n >= 0 && n < N;
+      const int m = ok ? (sk == 0 ? N - 1 - n : n) : 0;
+      dv[q] = drow[m];
+      ev[q] = ok ? ew[m] : 0.0;
     }
   };
   auto store = [&](int ch) {
 #pragma unroll
     for (int q = 0; q < kAcPer; ++q) {
       const int slot = (T0 - kAcChunk * (ch + 1) + 64 * q + lane) & (kAcRing - 1);
-      xs[slot] = sv[q];
-      xs[slot + kAcRing] = sv[q];
+      const double v = ev[q] * dv[q];
+      xs[slot] = v;
+      xs[slot + kAcRing] = v;
     }
   };
-  // thresholds are consumed in order; the next one is kept in a register
+  // snapshot records (threshold, band, K), consumed in order from an LDS copy
+  extern __shared__ SkSnap tab[];
+  for (int q = lane; q < B; q += 64) tab[q] = snaps[q];
+  __syncthreads();
   int k = 0;
-  int nextS = B > 0 ? thr[0].x : -1;
+  SkSnap cur = tab[0];
   auto snapshot = [&]() {
     double mine[NLPL];
-    diag_sums<NT, G, NLPL>(acc, ep, nlags, lane, mine);
-    const int j = thr[k].y;
-    const double K = ks[j];
+    if constexpr (SNAP) {
+      diag_sums<NT, G, NLPL>(acc, ep, nlags, lane, mine);
+    } else {  // timing experiment: keep every MFMA live through a cheap checksum
+      double cs = 0.0;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) cs += acc[t][0] + acc[t][1] + acc[t][2] + acc[t][3];
+#pragma unroll
+      for (int q = 0; q < NLPL; ++q) mine[q] = cs;
+    }
 #pragma unroll
     for (int q = 0; q < NLPL; ++q) {
       const int L = lane + 64 * q;
-      if (L < nlags) out[(int64_t)j * nlags + L] = K * mine[q];
+      if (L < nlags) out[(int64_t)cur.band * nlags + L] = cur.K * mine[q];
     }
     ++k;
-    nextS = k < B ? thr[k].x : -1;
+    cur = k < B ? tab[k] : SkSnap{-1, 0, 0.0};
   };
   auto step = [&](int P, int lo, int hi) {
     const int pa = P + 16 * kk_lane + i_lane;
@@ -690,10 +699,10 @@ __global__ __launch_bounds__(64, 2) void ac_sweep_kernel(DevConsts c, const doub
       const int P = T0 - kAcChunk * (ch + 1) + 64 * q;
       if ((P >> 6) < bmin) break;
       int hiM = P + 64;
-      while (nextS >= hiM) snapshot();
-      while (nextS > P) {
-        step(P, nextS, hiM);
-        hiM = nextS;
+      while (k < B && cur.S >= hiM) snapshot();
+      while (k < B && cur.S > P) {
+        step(P, cur.S, hiM);
+        hiM = cur.S;
         snapshot();
       }
       step(P, P, hiM);
@@ -788,15 +797,22 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
     int lb = e == 0 ? 0 : (e == 1 ? m1 : m2);
     lb = max(lb, b - (nlags - 1));
     if (lb >= b) continue;
+    constexpr int kSt = (kWin + 16 * NT + 63) / 64;  // B reads reach xb[kWin - 1 + 16 NT - 1]
+    double wv[kSt], dv[kSt];
+#pragma unroll
+    for (int u = 0; u < kSt; ++u) {  // all loads first: one exposed latency per boundary
+      const int pos = b - kWin + 64 * u + lane;
+      const int pm = pos < 0 ? 0 : (pos >= N ? pos - N : pos);
+      wv[u] = wrow[pm];
+      dv[u] = drow[pm];
+    }
     __syncthreads();
-    for (int q = lane; q < kWin + 16 * NT; q += 64) {  // B reads reach xb[kWin - 1 + 16 NT - 1]
+#pragma unroll
+    for (int u = 0; u < kSt; ++u) {
+      const int q = 64 * u + lane;
       const int pos = b - kWin + q;
-      double x = 0.0;
-      if (pos >= lb) {
-        const int pm = pos >= N ? pos - N : pos;
-        x = wrow[pm] * drow[pm];
-      }
-      xb[q] = pos >= b ? x : 0.0;
+      const double x = pos >= lb ? wv[u] * dv[u] : 0.0;
+      if (q < kWin + 16 * NT) xb[q] = pos >= b ? x : 0.0;
       if (q < kWin) xa[q] = pos < b ? x : 0.0;
     }
     __syncthreads();
@@ -1374,10 +1390,16 @@ template <int NT>
 static hipError_t launch_struct_nt(const DevConsts& c, const double* dct, int nframes, double* r, double* rup,
                                    hipStream_t s) {
   static const bool full = getenv("FDLP_SWEEP_FULL_EPI") != nullptr;
-  if (full)
-    hipLaunchKernelGGL((ac_sweep_kernel<NT, NT>), dim3(2 * nframes), dim3(64), 0, s, c, dct, r, rup);
+  static const bool nosnap = getenv("FDLP_SWEEP_NOSNAP") != nullptr;  // timing experiment only
+  const size_t tab = sizeof(SkSnap) * (size_t)c.B;
+  if (nosnap && full)
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, NT, false>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
+  else if (nosnap)
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, 4, false>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
+  else if (full)
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, NT>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
   else
-    hipLaunchKernelGGL((ac_sweep_kernel<NT, 4>), dim3(2 * nframes), dim3(64), 0, s, c, dct, r, rup);
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, 4>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
   hipLaunchKernelGGL(ac_band_kernel<NT>, dim3(nframes * c.B), dim3(64), 0, s, c, dct, r, rup);
   return hipGetLastError();
 }
@@ -1385,7 +1407,7 @@ static hipError_t launch_struct_nt(const DevConsts& c, const double* dct, int nf
 hipError_t launch_autocorr_structured(const DevConsts& c, const double* dct, int nframes, double* r,
                                       double* rup, hipStream_t s) {
   if (nframes <= 0) return hipSuccess;
-  if (!c.sk_e || !c.sk_thr || !c.sk_k || !c.sk_reg) return hipErrorInvalidValue;
+  if (!c.sk_e || !c.sk_snap || !c.sk_reg) return hipErrorInvalidValue;
   switch (autocorr_tiles(c.nlags)) {
 #define FDLP_ST_CASE(n) case n: return launch_struct_nt<n>(c, dct, nframes, r, rup, s);
     FDLP_ST_CASE(1) FDLP_ST_CASE(2) FDLP_ST_CASE(3) FDLP_ST_CASE(4) FDLP_ST_CASE(5)

@@ -109,8 +109,7 @@ std::vector<double> fbank_mel(int nf, int nfft, int srate, double wf, int* ncol_
 // E, E', K, K' must stay well inside the fp64 range.  Returns false otherwise (direct path).
 struct SkirtTables {
   std::vector<double> e;    // [2, N]
-  std::vector<int2> thr;    // [2, B]
-  std::vector<double> k;    // [2, B]
+  std::vector<fdlp::SkSnap> snap;  // [2, B] in sweep order
   std::vector<int2> reg;    // [B]
   int smin[2] = {0, 0};
 };
@@ -149,21 +148,22 @@ bool skirt_tables(const fdlp_config& c, int B, int N, int nfft, SkirtTables* T) 
     T->e[m] = (double)powl(10.0L, (long double)a * x);
     T->e[(size_t)N + m] = (double)powl(10.0L, -(long double)b * x);
   }
-  T->k.resize(2 * (size_t)B);
+  std::vector<double> K(2 * (size_t)B);
   for (int j = 0; j < B; ++j) {
     const long double ea = (long double)a * ((long double)om - 2.0L * cf[j] + 2.0L * c0);
     const long double eb = (long double)b * (2.0L * cf[j] + (long double)om - 2.0L * c0);
     if (fabsl(ea) > 150.0L || fabsl(eb) > 150.0L) return false;
-    T->k[j] = (double)powl(10.0L, ea);
-    T->k[(size_t)B + j] = (double)powl(10.0L, eb);
+    K[j] = (double)powl(10.0L, ea);
+    K[(size_t)B + j] = (double)powl(10.0L, eb);
   }
-  T->thr.resize(2 * (size_t)B);
+  T->snap.resize(2 * (size_t)B);
   for (int sk = 0; sk < 2; ++sk) {
-    std::vector<int2> t(B);
-    for (int j = 0; j < B; ++j) t[j] = make_int2(sk == 0 ? N - T->reg[j].x : T->reg[j].y, j);
-    std::stable_sort(t.begin(), t.end(), [](const int2& u, const int2& v) { return u.x > v.x; });
-    for (int j = 0; j < B; ++j) T->thr[(size_t)sk * B + j] = t[j];
-    T->smin[sk] = t[B - 1].x;
+    std::vector<fdlp::SkSnap> t(B);
+    for (int j = 0; j < B; ++j)
+      t[j] = fdlp::SkSnap{sk == 0 ? N - T->reg[j].x : T->reg[j].y, j, K[(size_t)sk * B + j]};
+    std::stable_sort(t.begin(), t.end(), [](const fdlp::SkSnap& u, const fdlp::SkSnap& v) { return u.S > v.S; });
+    for (int j = 0; j < B; ++j) T->snap[(size_t)sk * B + j] = t[j];
+    T->smin[sk] = t[B - 1].S;
   }
   return true;
 }
@@ -247,11 +247,15 @@ struct fdlp_plan {
   bool profiling = false;
   bool debug_intermediates = false;  // keep a/gg/cep of the fused LPC kernel for fdlp_debug_fetch
   bool fused = false;                // autocorrelation + LPC tail in one kernel (FDLP_FUSE_TAIL=1)
+  int pipeline = 1;                  // sub-batches alternated over two streams (FDLP_PIPELINE)
+  hipStream_t aux_stream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool sk_avail = false;             // structured autocorrelation possible for this filterbank
   int ac_path = FDLP_AC_DIRECT;      // FDLP_AC_DIRECT or FDLP_AC_STRUCTURED
   SkirtTables sk;
-  double *d_sk_e = nullptr, *d_sk_k = nullptr, *r_up = nullptr;
-  int2 *d_sk_thr = nullptr, *d_sk_reg = nullptr;
+  double *d_sk_e = nullptr, *r_up = nullptr;
+  fdlp::SkSnap* d_sk_snap = nullptr;
+  int2* d_sk_reg = nullptr;
   std::vector<std::vector<hipEvent_t>> prof_pending;
   double prof_ms[FDLP_NUM_STAGES] = {0};
   int prof_calls = 0;
@@ -260,13 +264,19 @@ struct fdlp_plan {
 namespace {
 
 int drain_profile(fdlp_plan* p) {
+  // per call: 5 events per sub-batch (stage 0..3 boundaries on its stream) + 2 around the OLA
   for (auto& ev : p->prof_pending) {
     HIP_TRY(hipEventSynchronize(ev.back()));
-    for (int k = 0; k < FDLP_NUM_STAGES; ++k) {
-      float ms = 0.f;
-      HIP_TRY(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
-      p->prof_ms[k] += ms;
-    }
+    const size_t nsub = (ev.size() - 2) / 5;
+    for (size_t i = 0; i < nsub; ++i)
+      for (int k = 0; k < 4; ++k) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, ev[5 * i + k], ev[5 * i + k + 1]));
+        p->prof_ms[k] += ms;
+      }
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, ev[ev.size() - 2], ev[ev.size() - 1]));
+    p->prof_ms[4] += ms;
     p->prof_calls++;
     for (auto e : ev) (void)hipEventDestroy(e);
   }
@@ -280,13 +290,16 @@ int free_plan(fdlp_plan* p) {
     for (auto e : ev) (void)hipEventDestroy(e);
   void* devs[] = {p->d_fbank, p->d_hamming, p->d_weights, p->d_env_cos, p->d_env_win, p->d_tw1, p->d_post,
                   p->d_om1, p->d_om2, p->d_lo, p->d_hi, p->ws.z, p->ws.dct, p->ws.r, p->ws.a, p->ws.gg,
-                  p->ws.cep, p->ws.env, p->d_frames, p->d_utts, p->d_sk_e, p->d_sk_k, p->r_up,
-                  p->d_sk_thr, p->d_sk_reg};
+                  p->ws.cep, p->ws.env, p->d_frames, p->d_utts, p->d_sk_e, p->r_up, p->d_sk_snap,
+                  p->d_sk_reg};
   for (void* d : devs)
     if (d) (void)hipFree(d);
   if (p->h_frames) (void)hipHostFree(p->h_frames);
   if (p->h_utts) (void)hipHostFree(p->h_utts);
   if (p->staging_done) (void)hipEventDestroy(p->staging_done);
+  if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
+  if (p->ev_join) (void)hipEventDestroy(p->ev_join);
+  if (p->aux_stream) (void)hipStreamDestroy(p->aux_stream);
   delete p;
   return FDLP_OK;
 }
@@ -426,6 +439,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
 
   p->sk_avail = skirt_tables(c, p->B, p->N, p->nfft, &p->sk);
   p->ac_path = p->sk_avail && getenv("FDLP_AUTOCORR_DIRECT") == nullptr ? FDLP_AC_STRUCTURED : FDLP_AC_DIRECT;
+  if (const char* e = getenv("FDLP_PIPELINE")) p->pipeline = std::max(1, atoi(e));
 
   // modulation weights (:94-118)
   const int M = p->M;
@@ -508,10 +522,9 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   d.env_cos = p->d_env_cos; d.env_win = p->d_env_win; d.tw1 = p->d_tw1; d.post = p->d_post;
   if (p->sk_avail) {
     PLAN_TRY(upload(&p->d_sk_e, p->sk.e.data(), p->sk.e.size()));
-    PLAN_TRY(upload(&p->d_sk_k, p->sk.k.data(), p->sk.k.size()));
-    PLAN_TRY(upload(&p->d_sk_thr, p->sk.thr.data(), p->sk.thr.size()));
+    PLAN_TRY(upload(&p->d_sk_snap, p->sk.snap.data(), p->sk.snap.size()));
     PLAN_TRY(upload(&p->d_sk_reg, p->sk.reg.data(), p->sk.reg.size()));
-    d.sk_e = p->d_sk_e; d.sk_k = p->d_sk_k; d.sk_thr = p->d_sk_thr; d.sk_reg = p->d_sk_reg;
+    d.sk_e = p->d_sk_e; d.sk_snap = p->d_sk_snap; d.sk_reg = p->d_sk_reg;
     d.sk_min[0] = p->sk.smin[0]; d.sk_min[1] = p->sk.smin[1];
   }
 
@@ -530,7 +543,10 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
       hipMalloc((void**)&p->d_utts, sizeof(fdlp::UttDesc) * F) != hipSuccess ||
       hipHostMalloc((void**)&p->h_frames, sizeof(fdlp::FrameDesc) * F, hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc((void**)&p->h_utts, sizeof(fdlp::UttDesc) * F, hipHostMallocDefault) != hipSuccess ||
-      hipEventCreateWithFlags(&p->staging_done, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&p->staging_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&p->aux_stream, hipStreamNonBlocking) != hipSuccess)
     PLAN_FAIL(FDLP_E_NOMEM, "workspace allocation failed (reduce max_frames)");
 #undef PLAN_FAIL
 #undef PLAN_TRY
@@ -661,45 +677,73 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
   p->staging_pending = true;
 
   const int items = (int)nf * p->B;
+  // Sub-batches alternate between the caller's stream and the plan's second stream so that the
+  // MFMA-bound autocorrelation of one overlaps the VALU-bound DFT / LPC kernels of the other.
+  const int nsub = (int)std::max<int64_t>(1, std::min<int64_t>(p->pipeline, nf / 256));
   std::vector<hipEvent_t> ev;
   if (p->profiling) {
     if (p->prof_pending.size() >= 64) {
       int rc = drain_profile(p);
       if (rc != FDLP_OK) return rc;
     }
-    ev.resize(FDLP_NUM_STAGES + 1);
+    ev.resize(5 * (size_t)nsub + 2);
     for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
   }
-  auto mark = [&](int k) -> hipError_t { return p->profiling ? hipEventRecord(ev[k], s) : hipSuccess; };
-  HIP_TRY(mark(0));
-  HIP_TRY(fdlp::launch_frames_dft1(p->dc, p->d1, p->d2.n, b->pcm_dev,
-                                   b->preprocess == FDLP_PRE_DIFF ? 2 : b->pcm_kind, b->noise_dev, p->d_frames,
-                                   nullptr, (int)nf, p->ws.z, p->d_om1, s));
-  HIP_TRY(mark(1));
-  HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z, (int)nf, p->ws.dct, p->d_om2, s));
-  HIP_TRY(mark(2));
-  if (p->ac_path == FDLP_AC_STRUCTURED) {
-    HIP_TRY(fdlp::launch_autocorr_structured(p->dc, p->ws.dct, (int)nf, p->ws.r, p->r_up, s));
+  // frames [f0, f0 + n) of sub-batch i: everything up to the envelopes is independent per frame
+  auto run_frames = [&](int i, int64_t f0, int n, hipStream_t st) -> int {
+    auto mark = [&](int k) -> hipError_t { return p->profiling ? hipEventRecord(ev[5 * i + k], st) : hipSuccess; };
+    const size_t N = (size_t)p->N, B = (size_t)p->B, nl = (size_t)p->nlags;
+    const size_t it0 = (size_t)f0 * B;
+    const int its = n * p->B;
+    double* r = p->ws.r + it0 * nl;
+    double* env = p->ws.env + it0 * p->kk;
+    double* a_dbg = p->debug_intermediates ? p->ws.a + it0 * (p->p + 1) : nullptr;
+    double* gg_dbg = p->debug_intermediates ? p->ws.gg + it0 : nullptr;
+    double* cep_dbg = p->debug_intermediates ? p->ws.cep + it0 * p->M : nullptr;
+    HIP_TRY(mark(0));
+    HIP_TRY(fdlp::launch_frames_dft1(p->dc, p->d1, p->d2.n, b->pcm_dev,
+                                     b->preprocess == FDLP_PRE_DIFF ? 2 : b->pcm_kind, b->noise_dev, p->d_frames + f0,
+                                     nullptr, n, p->ws.z + f0 * N, p->d_om1, st));
+    HIP_TRY(mark(1));
+    HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z + f0 * N, n, p->ws.dct + f0 * N, p->d_om2, st));
+    HIP_TRY(mark(2));
+    if (p->ac_path == FDLP_AC_STRUCTURED) {
+      HIP_TRY(fdlp::launch_autocorr_structured(p->dc, p->ws.dct + f0 * N, n, r, p->r_up + it0 * nl, st));
+    } else if (p->fused && !p->debug_intermediates) {
+      // autocorrelation + LPC tail in one launch (stage 3 is then empty)
+      HIP_TRY(fdlp::launch_band_fused(p->dc, p->cfg.odd_mod_zero, p->ws.dct + f0 * N, its, r, env, st));
+      HIP_TRY(mark(3));
+      HIP_TRY(mark(4));
+      return FDLP_OK;
+    } else {
+      HIP_TRY(fdlp::launch_autocorr(p->dc, p->ws.dct + f0 * N, nullptr, its, r, st));
+    }
     HIP_TRY(mark(3));
-    HIP_TRY(fdlp::launch_lpc_env(p->dc, p->cfg.odd_mod_zero, p->ws.r, items, p->ws.env,
-                                 p->debug_intermediates ? p->ws.a : nullptr, p->debug_intermediates ? p->ws.gg : nullptr,
-                                 p->debug_intermediates ? p->ws.cep : nullptr, s));
-  } else if (p->fused && !p->debug_intermediates) {
-    // autocorrelation + LPC tail in one launch (stage 3 is then empty)
-    HIP_TRY(fdlp::launch_band_fused(p->dc, p->cfg.odd_mod_zero, p->ws.dct, items, p->ws.r, p->ws.env, s));
-    HIP_TRY(mark(3));
+    HIP_TRY(fdlp::launch_lpc_env(p->dc, p->cfg.odd_mod_zero, r, its, env, a_dbg, gg_dbg, cep_dbg, st));
+    HIP_TRY(mark(4));
+    return FDLP_OK;
+  };
+  if (nsub == 1) {
+    int rc = run_frames(0, 0, (int)nf, s);
+    if (rc != FDLP_OK) return rc;
   } else {
-    HIP_TRY(fdlp::launch_autocorr(p->dc, p->ws.dct, nullptr, items, p->ws.r, s));
-    HIP_TRY(mark(3));
-    HIP_TRY(fdlp::launch_lpc_env(p->dc, p->cfg.odd_mod_zero, p->ws.r, items, p->ws.env,
-                                 p->debug_intermediates ? p->ws.a : nullptr, p->debug_intermediates ? p->ws.gg : nullptr,
-                                 p->debug_intermediates ? p->ws.cep : nullptr, s));
+    HIP_TRY(hipEventRecord(p->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(p->aux_stream, p->ev_fork, 0));
+    for (int i = 0; i < nsub; ++i) {
+      const int64_t f0 = nf * i / nsub, f1 = nf * (i + 1) / nsub;
+      int rc = run_frames(i, f0, (int)(f1 - f0), (i & 1) ? p->aux_stream : s);
+      if (rc != FDLP_OK) return rc;
+    }
+    HIP_TRY(hipEventRecord(p->ev_join, p->aux_stream));
+    HIP_TRY(hipStreamWaitEvent(s, p->ev_join, 0));
   }
-  HIP_TRY(mark(4));
+  if (p->profiling) HIP_TRY(hipEventRecord(ev[ev.size() - 2], s));
   HIP_TRY(fdlp::launch_ola_log(p->dc, p->ws.env, p->d_frames, p->d_utts, b->n_utt, maxL, b->out_dev,
                                b->out_f64_dev, b->ark_decimals, s));
-  HIP_TRY(mark(5));
-  if (p->profiling) p->prof_pending.push_back(ev);
+  if (p->profiling) {
+    HIP_TRY(hipEventRecord(ev.back(), s));
+    p->prof_pending.push_back(ev);
+  }
   return FDLP_OK;
 }
 
@@ -716,6 +760,22 @@ int fdlp_set_autocorr_path(fdlp_plan* p, int32_t path) {
   } else {
     return fail(FDLP_E_INVALID, "fdlp_set_autocorr_path: unknown path");
   }
+  return FDLP_OK;
+}
+
+int fdlp_plan_regions(const fdlp_plan* p, int32_t* m1, int32_t* m2) {
+  if (!p) return fail(FDLP_E_INVALID, "fdlp_plan_regions: null plan");
+  if (!p->sk_avail) return fail(FDLP_E_INVALID, "filterbank has no skirt/flat-top split (structured path unavailable)");
+  for (int j = 0; j < p->B; ++j) {
+    if (m1) m1[j] = p->sk.reg[j].x;
+    if (m2) m2[j] = p->sk.reg[j].y;
+  }
+  return FDLP_OK;
+}
+
+int fdlp_set_pipeline(fdlp_plan* p, int32_t n_sub) {
+  if (!p || n_sub < 1) return fail(FDLP_E_INVALID, "fdlp_set_pipeline: need a plan and n_sub >= 1");
+  p->pipeline = n_sub;
   return FDLP_OK;
 }
 

@@ -234,6 +234,16 @@ class FdlpPlan:
     def set_autocorr_path(self, path: str = "auto"):
         check(lib.fdlp_set_autocorr_path(self._h, self.AUTOCORR_PATHS[path]))
 
+    def regions(self):
+        """(m1, m2) int32 arrays: band j's lower skirt [0,m1), flat top [m1,m2), upper skirt [m2,N)."""
+        m1 = np.empty(self.B, dtype=np.int32)
+        m2 = np.empty(self.B, dtype=np.int32)
+        check(lib.fdlp_plan_regions(self._h, ptr(m1, ctypes.c_int32), ptr(m2, ctypes.c_int32)))
+        return m1, m2
+
+    def set_pipeline(self, n_sub: int):
+        check(lib.fdlp_set_pipeline(self._h, int(n_sub)))
+
     def set_debug(self, keep_intermediates: bool = True):
         check(lib.fdlp_set_debug(self._h, int(bool(keep_intermediates))))
 

@@ -178,3 +178,23 @@ def test_structured_autocorr_matches_oracle(fb, nf, fd, order, cn):
         O.FdlpOracle(ocfg).band_envelopes(x, keep)
         rel = np.abs(d["r"] - keep.r).max(axis=-1) / np.abs(keep.r[..., 0])
         assert rel.max() <= 1e-12, rel.max()
+
+
+def test_pipelined_sub_batches_match_serial():
+    """Sub-batches on two streams (fdlp_set_pipeline) give bit-identical features."""
+    from speech_recognition_tools_amd import FdlpPlan, FeatureConfig, PyRandom
+    rng = np.random.default_rng(5)
+    lens = [int(v) for v in rng.integers(8000, 300000, size=200)]
+    pcm = (rng.standard_normal(sum(lens)) * 2000).astype(np.int16)
+    plan = FdlpPlan(FeatureConfig.wsj(), device=0, max_frames=4096)
+    nj = sum(plan.geometry(T)[0] - 1 for T in lens)
+    assert sum(plan.geometry(T)[0] for T in lens) >= 1024
+    jit = PyRandom(3).randbits2(nj)
+    res = []
+    for n in (1, 2, 4):
+        plan.set_pipeline(n)
+        out, rows, out64 = plan.compute(torch.from_numpy(pcm).cuda(), lens, jit, want_f64=True)
+        torch.cuda.synchronize()
+        res.append(out64.cpu().numpy())
+    np.testing.assert_array_equal(res[0], res[1])
+    np.testing.assert_array_equal(res[0], res[2])
