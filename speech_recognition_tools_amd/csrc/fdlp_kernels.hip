@@ -589,6 +589,50 @@ __device__ __forceinline__ void diag_sums(const dbl4* acc, double* ep, int nlags
   }
 }
 
+// Diagonal sums in lag blocks of LB lags (LB = 32 or 64), branch-free.  Block g covers lags
+// [LB g, LB g + LB); its 16-term sums touch tiles LB/16 g .. LB/16 (g+1), which are written whole
+// into a padded lag-major image (rows = lags LB g - 15 .. LB g + LB + 14, stride 17).  LPL = 64/LB
+// lanes share a lag, each adding 16/LPL consecutive terms, and a DPP swap finishes the sum; the
+// first lane of each group calls emit(L, r_L).  ep holds (LB + 31) * 17 doubles.  Block = one wave.
+template <int NT, int LB, typename Emit>
+__device__ __forceinline__ void diag_blocks(const dbl4* acc, double* ep, int nlags, int lane, Emit emit) {
+  static_assert(LB == 32 || LB == 64, "lag block");
+  constexpr int LPL = 64 / LB;
+  constexpr int TPB = LB / 16;                       // tiles per block (+1 shared with the next)
+  constexpr int NB = (16 * NT + LB - 1) / LB;
+  const int col = lane & 15;
+  const int row0 = lane >> 4;
+  const int m = lane / LPL;
+  const int part = lane % LPL;
+#pragma unroll
+  for (int g = 0; g < NB; ++g) {
+    if (LB * g >= nlags) break;
+#pragma unroll
+    for (int u = 0; u <= TPB; ++u) {
+      const int t = TPB * g + u;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + 4 * r;
+        // lag 16 t + col - row -> image row (lag - LB g + 15)
+        const double v = t < NT ? acc[t < NT ? t : 0][r] : 0.0;
+        ep[(16 * u + col - row + 15) * 17 + row] = v;
+      }
+    }
+    wave_lds_sync();
+    const double* src = ep + (m + 15) * 17 + part * (16 / LPL);
+    double v[16 / LPL];
+#pragma unroll
+    for (int i = 0; i < 16 / LPL; ++i) v[i] = src[i];
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16 / LPL; ++i) sum += v[i];
+    if constexpr (LPL == 2) sum += dpp_f64<0xB1>(sum);  // quad_perm [1,0,3,2]: partner lane
+    const int L = LB * g + m;
+    if (part == 0 && L < nlags) emit(L, sum);
+    wave_lds_sync();
+  }
+}
+
 // One MFMA k-step of the lag tiles: A = x[P + 16 kk + i] (masked to [lo, hi)), B_t = x[P + 16(kk+t) + jj]
 // read from a window w (w points at the lane's A element; B_t is w[16 t]).
 template <int NT>
@@ -608,8 +652,7 @@ template <int NT, int G, bool SNAP = true>
 __global__ __launch_bounds__(64, 2) void ac_sweep_kernel(DevConsts c, const double* __restrict__ dct,
                                                          double* __restrict__ rlow, double* __restrict__ rup) {
   static_assert(16 * NT <= kAcChunk, "window halo must fit one chunk");
-  constexpr int NLPL = (16 * NT + 63) / 64;
-  constexpr int kEpi = (16 * G + 15) * 17;
+  constexpr int kEpi = (G + 31) * 17;  // G = lag block of diag_blocks
   __shared__ double xs[2 * kAcRing];
   __shared__ double ep[kEpi];
 
@@ -661,20 +704,15 @@ __global__ __launch_bounds__(64, 2) void ac_sweep_kernel(DevConsts c, const doub
   int k = 0;
   SkSnap cur = tab[0];
   auto snapshot = [&]() {
-    double mine[NLPL];
+    double* o = out + (int64_t)cur.band * nlags;
+    const double K = cur.K;
     if constexpr (SNAP) {
-      diag_sums<NT, G, NLPL>(acc, ep, nlags, lane, mine);
+      diag_blocks<NT, G>(acc, ep, nlags, lane, [&](int L, double v) { o[L] = K * v; });
     } else {  // timing experiment: keep every MFMA live through a cheap checksum
       double cs = 0.0;
 #pragma unroll
       for (int t = 0; t < NT; ++t) cs += acc[t][0] + acc[t][1] + acc[t][2] + acc[t][3];
-#pragma unroll
-      for (int q = 0; q < NLPL; ++q) mine[q] = cs;
-    }
-#pragma unroll
-    for (int q = 0; q < NLPL; ++q) {
-      const int L = lane + 64 * q;
-      if (L < nlags) out[(int64_t)cur.band * nlags + L] = cur.K * mine[q];
+      if (lane < nlags) o[lane] = K * cs;
     }
     ++k;
     cur = k < B ? tab[k] : SkSnap{-1, 0, 0.0};
@@ -723,11 +761,9 @@ template <int NT>
 __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const double* __restrict__ dct,
                                                         double* __restrict__ r, const double* __restrict__ rup) {
   static_assert(16 * NT <= kAcChunk, "window halo must fit one chunk");
-  constexpr int G = 2;
-  constexpr int NLPL = (16 * NT + 63) / 64;
-  constexpr int kEpi = (16 * G + 15) * 17;
+  constexpr int kEpi = (32 + 31) * 17;                   // diag_blocks<NT, 32> image
   constexpr int kWin = (16 * NT + 63) / 64 * 64;         // A window of a straddle (>= nlags - 1)
-  constexpr int kLds = 2 * kAcRing;
+  constexpr int kLds = 2 * kAcRing > kEpi ? 2 * kAcRing : kEpi;
   static_assert(kEpi <= kLds && 2 * kWin + 16 * NT <= kLds, "LDS regions");
   __shared__ double xs[kLds];
 
@@ -827,16 +863,9 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
     }
   }
   __syncthreads();
-  double mine[NLPL];
-  diag_sums<NT, G, NLPL>(acc, xs, nlags, lane, mine);
-#pragma unroll
-  for (int q = 0; q < NLPL; ++q) {
-    const int L = lane + 64 * q;
-    if (L < nlags) {
-      const int64_t o = (int64_t)item * nlags + L;
-      r[o] = mine[q] + r[o] + rup[o];
-    }
-  }
+  double* ro = r + (int64_t)item * nlags;
+  const double* uo = rup + (int64_t)item * nlags;
+  diag_blocks<NT, 32>(acc, xs, nlags, lane, [&](int L, double v) { ro[L] = v + ro[L] + uo[L]; });
 }
 
 template <int NT>
@@ -1393,13 +1422,13 @@ static hipError_t launch_struct_nt(const DevConsts& c, const double* dct, int nf
   static const bool nosnap = getenv("FDLP_SWEEP_NOSNAP") != nullptr;  // timing experiment only
   const size_t tab = sizeof(SkSnap) * (size_t)c.B;
   if (nosnap && full)
-    hipLaunchKernelGGL((ac_sweep_kernel<NT, NT, false>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, 64, false>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
   else if (nosnap)
-    hipLaunchKernelGGL((ac_sweep_kernel<NT, 4, false>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, 32, false>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
   else if (full)
-    hipLaunchKernelGGL((ac_sweep_kernel<NT, NT>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, 64>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
   else
-    hipLaunchKernelGGL((ac_sweep_kernel<NT, 4>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, 32>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
   hipLaunchKernelGGL(ac_band_kernel<NT>, dim3(nframes * c.B), dim3(64), 0, s, c, dct, r, rup);
   return hipGetLastError();
 }
