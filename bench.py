@@ -68,6 +68,28 @@ def cpu_baseline(cfg_name, T, workers, per_worker):
                        (workers * per_worker, T / 16000.0, per_worker))
 
 
+PMC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc.json")
+AC_KERNEL_PREFIX = {"structured": ("fdlp::ac_sweep_kernel", "fdlp::ac_band_kernel"),
+                    "direct": ("fdlp::autocorr_kernel",)}
+
+
+def stage_traffic(path):
+    """HBM bytes per launch of the autocorrelation stage from the committed rocprofv3 PMC summary
+    of this same bench command (scripts/round_evidence.sh -> scripts/pmc_report.py): FETCH_SIZE x 2
+    (gfx950 correction, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, KiB -> bytes.  None if absent."""
+    try:
+        rows = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None
+    tot, seen = 0.0, 0
+    for name, m in rows.items():
+        short = name.replace("void ", "")
+        if short.startswith(AC_KERNEL_PREFIX[path]) and "fetch_bytes_x2" in m and "write_bytes" in m:
+            tot += m["fetch_bytes_x2"] + m["write_bytes"]
+            seen += 1
+    return tot if seen == len(AC_KERNEL_PREFIX[path]) else None
+
+
 AC_KERNELS = {"structured": "autocorr stage: ac_sweep_kernel + ac_band_kernel (v_mfma_f64_16x16x4f64)",
               "direct": "autocorr stage: autocorr_kernel (v_mfma_f64_16x16x4f64)"}
 
@@ -194,7 +216,8 @@ def main():
                    "parallelism": "scp-shard x%d (no collective)" % world},
         "roofline": {"bound": "mfma", "kernel": AC_KERNELS[plan.autocorr_path],
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": stage_traffic(plan.autocorr_path),
+                     "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/r01_pmc.json)",
                      "avg_launch_ms": ac_ms, "algorithmic_flops_per_launch": flops_per_launch},
         "stage_ms_per_step": {k: v / max(ncalls, 1) for k, v in stages.items()},
         "cpu_baseline": cpu,
