@@ -589,6 +589,16 @@ __device__ __forceinline__ void diag_sums(const dbl4* acc, double* ep, int nlags
   }
 }
 
+// Workgroup b is dispatched to XCD b % 8.  Giving every XCD a contiguous run of work items keeps
+// the items that read the same frame (its D row) on one L2 instead of pulling the row into all
+// eight.  Grid = 8 * ceil(total / 8); the padding workgroups get an index >= total.
+constexpr int kXcds = 8;
+__device__ __forceinline__ int xcd_item() {
+  const int per = gridDim.x / kXcds;
+  return (int)(blockIdx.x % kXcds) * per + (int)(blockIdx.x / kXcds);
+}
+static inline int xcd_grid(int total) { return (total + kXcds - 1) / kXcds * kXcds; }
+
 // Diagonal sums in lag blocks of LB lags (LB = 32 or 64), branch-free.  Block g covers lags
 // [LB g, LB g + LB); its 16-term sums touch tiles LB/16 g .. LB/16 (g+1), which are written whole
 // into a padded lag-major image (rows = lags LB g - 15 .. LB g + LB + 14, stride 17).  LPL = 64/LB
@@ -650,14 +660,17 @@ __device__ __forceinline__ void lag_step(dbl4* acc, const double* w, bool keep) 
 // A threshold inside a k-step splits it into two A-masked steps around the snapshot.
 template <int NT, int G, bool SNAP = true>
 __global__ __launch_bounds__(64, 2) void ac_sweep_kernel(DevConsts c, const double* __restrict__ dct,
-                                                         double* __restrict__ rlow, double* __restrict__ rup) {
+                                                         double* __restrict__ rlow, double* __restrict__ rup,
+                                                         int nwork) {
   static_assert(16 * NT <= kAcChunk, "window halo must fit one chunk");
   constexpr int kEpi = (G + 31) * 17;  // G = lag block of diag_blocks
   __shared__ double xs[2 * kAcRing];
   __shared__ double ep[kEpi];
 
-  const int f = blockIdx.x >> 1;
-  const int sk = blockIdx.x & 1;
+  const int w = xcd_item();  // (frame, skirt) pairs of a frame stay on one XCD
+  if (w >= nwork) return;
+  const int f = w >> 1;
+  const int sk = w & 1;
   const int lane = threadIdx.x;
   const int N = c.N, B = c.B, nlags = c.nlags;
   const double* drow = dct + (int64_t)f * N;
@@ -759,7 +772,8 @@ __global__ __launch_bounds__(64, 2) void ac_sweep_kernel(DevConsts c, const doub
 // r holds the lower-skirt term on entry and r_j on exit.
 template <int NT>
 __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const double* __restrict__ dct,
-                                                        double* __restrict__ r, const double* __restrict__ rup) {
+                                                        double* __restrict__ r, const double* __restrict__ rup,
+                                                        int items) {
   static_assert(16 * NT <= kAcChunk, "window halo must fit one chunk");
   constexpr int kEpi = (32 + 31) * 17;                   // diag_blocks<NT, 32> image
   constexpr int kWin = (16 * NT + 63) / 64 * 64;         // A window of a straddle (>= nlags - 1)
@@ -767,7 +781,8 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
   static_assert(kEpi <= kLds && 2 * kWin + 16 * NT <= kLds, "LDS regions");
   __shared__ double xs[kLds];
 
-  const int item = blockIdx.x;
+  const int item = xcd_item();  // the B bands of a frame run on one XCD
+  if (item >= items) return;
   const int lane = threadIdx.x;
   const int N = c.N, nlags = c.nlags;
   const int f = item / c.B, j = item % c.B;
@@ -1422,14 +1437,14 @@ static hipError_t launch_struct_nt(const DevConsts& c, const double* dct, int nf
   static const bool nosnap = getenv("FDLP_SWEEP_NOSNAP") != nullptr;  // timing experiment only
   const size_t tab = sizeof(SkSnap) * (size_t)c.B;
   if (nosnap && full)
-    hipLaunchKernelGGL((ac_sweep_kernel<NT, 64, false>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, 64, false>), dim3(xcd_grid(2 * nframes)), dim3(64), tab, s, c, dct, r, rup, 2 * nframes);
   else if (nosnap)
-    hipLaunchKernelGGL((ac_sweep_kernel<NT, 32, false>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, 32, false>), dim3(xcd_grid(2 * nframes)), dim3(64), tab, s, c, dct, r, rup, 2 * nframes);
   else if (full)
-    hipLaunchKernelGGL((ac_sweep_kernel<NT, 64>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, 64>), dim3(xcd_grid(2 * nframes)), dim3(64), tab, s, c, dct, r, rup, 2 * nframes);
   else
-    hipLaunchKernelGGL((ac_sweep_kernel<NT, 32>), dim3(2 * nframes), dim3(64), tab, s, c, dct, r, rup);
-  hipLaunchKernelGGL(ac_band_kernel<NT>, dim3(nframes * c.B), dim3(64), 0, s, c, dct, r, rup);
+    hipLaunchKernelGGL((ac_sweep_kernel<NT, 32>), dim3(xcd_grid(2 * nframes)), dim3(64), tab, s, c, dct, r, rup, 2 * nframes);
+  hipLaunchKernelGGL(ac_band_kernel<NT>, dim3(xcd_grid(nframes * c.B)), dim3(64), 0, s, c, dct, r, rup, nframes * c.B);
   return hipGetLastError();
 }
 
