@@ -257,8 +257,9 @@ __device__ __forceinline__ double wave_sum(double v) {
 // -----------------------------------------------------------------------------------------
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  // every control used here has an in-row source for every lane, so no 'old' value is needed
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
 // sum over the 16 lanes of a DPP row; every lane gets the same (bitwise) value
@@ -1175,23 +1176,32 @@ struct LpcEnvArgs {
 
 // Durbin recursion with a[] resident in LDS (la[0..p], zero beyond) and r in LDS (lr): lane l of
 // the 16-lane row sums a_i r_{k-i} over i = l+1, l+17, ... and updates the symmetric pairs
-// (a_i, a_{k-i}) in place, so no mirror copy and no per-slot predicates are needed.  Returns gg.
+// (a_i, a_{k-i}) in place, so no mirror copy is needed.  Both loops run a uniform trip count: the
+// a_i with i >= k are still zero and lr[-15..-1] is the zero tail of la, so the extra terms vanish.
+// 1/E comes from v_rcp_f64 and two Newton steps.  Returns gg.
 __device__ __forceinline__ double durbin16(double* la, const double* lr, int p, int l) {
   double E = lr[0];
   for (int k = 1; k <= p; ++k) {
+    const int S = (k + 14) >> 4;
     double part = 0.0;
-    for (int i = l + 1; i < k; i += 16) part += la[i] * lr[k - i];
+    for (int s = 0; s < S; ++s) {
+      const int i = l + 1 + 16 * s;
+      part = fma(la[i], lr[k - i], part);
+    }
     const double acc = lr[k] + row_sum16(part);
-    const double kappa = -acc / E;
+    double rE = __builtin_amdgcn_rcp(E);
+    rE = fma(rE, fma(-E, rE, 1.0), rE);
+    rE = fma(rE, fma(-E, rE, 1.0), rE);
+    const double kappa = -acc * rE;
     wave_lds_sync();
-    for (int i = l + 1; 2 * i <= k; i += 16) {
-      const int j = k - i;
-      const double ai = la[i], aj = la[j];
-      if (i == j) {
-        la[i] = ai + kappa * ai;
-      } else {
-        la[i] = ai + kappa * aj;
-        la[j] = aj + kappa * ai;
+    const int S2 = (k + 31) >> 5;
+    for (int s = 0; s < S2; ++s) {
+      const int i = l + 1 + 16 * s;
+      if (2 * i <= k) {  // i == k - i writes the same value twice
+        const int j = k - i;
+        const double ai = la[i], aj = la[j];
+        la[i] = fma(kappa, aj, ai);
+        la[j] = fma(kappa, ai, aj);
       }
     }
     if (l == 0) la[k] = kappa;
@@ -1199,8 +1209,25 @@ __device__ __forceinline__ double durbin16(double* la, const double* lr, int p, 
     E = E * (1.0 - kappa * kappa);
   }
   double part = 0.0;
-  for (int i = l; i <= p; i += 16) part += la[i] * lr[i + 1];
+  for (int i = l; i <= p; i += 16) part = fma(la[i], lr[i + 1], part);
   return lr[0] + row_sum16(part);
+}
+
+// In-block part of the cepstrum recurrence for coefficient b0 + KK: lane KK finishes c_{b0+KK},
+// DPP row_newbcast hands it to the row, the later lanes of the block fold it in.
+template <int KK>
+__device__ __forceinline__ void cep_block_step(int b0, int M, int l, double gg, double inv_n, const double* la,
+                                               int n, double& acc, double& mine) {
+  const int kg = b0 + KK;
+  if (kg >= M) return;
+  if (l == KK) {
+    if (kg == 0) mine = log(sqrt(gg));
+    else if (kg == 1) mine = -la[1];
+    else mine = -la[kg] - acc * inv_n;
+  }
+  const double ck = dpp_f64<0x150 + KK>(mine);  // row_newbcast:KK
+  if (kg >= 1 && l > KK) acc = fma((double)kg * ck, la[n - kg], acc);
+  if constexpr (KK + 1 < 16) cep_block_step<KK + 1>(b0, M, l, gg, inv_n, la, n, acc, mine);
 }
 
 template <int TS>
@@ -1224,7 +1251,9 @@ __global__ __launch_bounds__(64) void lpc_env_kernel(LpcEnvArgs A) {
     if (l == 0) A.gg_out[item] = gg;
   }
   wave_lds_sync();
-  // ---- phase 2: cepstrum (features.py:233-246), alpha_n = -la[n] --------------------------
+  // ---- phase 2: cepstrum (features.py:233-246): c_n = -a_n - sum_{k<n} (k/n) c_k a_{n-k} --------
+  // blocks of 16 coefficients: the finished blocks enter as a lane-parallel dot product, the block
+  // itself as a 16-step recurrence with the new c_k broadcast along the row.
   double* cs = lr;
   for (int b0 = 0; b0 < M; b0 += 16) {
     const int n = b0 + l;
@@ -1232,19 +1261,9 @@ __global__ __launch_bounds__(64) void lpc_env_kernel(LpcEnvArgs A) {
     double acc = 0.0;
     const int kstart = max(1, b0 - p);
     double kd = (double)kstart;
-    for (int k = kstart; k < b0; ++k, kd += 1.0) acc -= ((kd * inv_n) * la[n - k]) * cs[k];
+    for (int k = kstart; k < b0; ++k, kd += 1.0) acc = fma(kd * cs[k], la[n - k], acc);
     double mine = 0.0;
-    for (int kk = 0; kk < 16; ++kk) {
-      const int kg = b0 + kk;
-      if (kg >= M) break;
-      if (l == kk) {
-        if (kg == 0) mine = log(sqrt(gg));
-        else if (kg == 1) mine = -la[1];
-        else mine = acc - la[kg];
-      }
-      const double ck = __shfl(mine, (g << 4) + kk, 64);
-      if (kg >= 1 && l > kk) acc -= (((double)kg * inv_n) * la[n - kg]) * ck;
-    }
+    cep_block_step<0>(b0, M, l, gg, inv_n, la, n, acc, mine);
     if (n < M) {
       cs[n] = mine;
       if (valid && A.cep_out) A.cep_out[(int64_t)item * M + n] = mine;
@@ -1265,35 +1284,47 @@ __global__ __launch_bounds__(64) void lpc_env_kernel(LpcEnvArgs A) {
     cw[n] = v;
   }
   wave_lds_sync();
-  // sum_n cw_n cos(n theta_t) with the Chebyshev recurrence cos((n+1)t) = 2 cos t cos(nt) - cos((n-1)t)
-  double sum[TS], cprev[TS], ccur[TS], c2[TS];
+  // S(t) = sum_n cw_n cos(n pi t / H), H = env_nfft / 2.  With u = min(t, H - t):
+  //   S(u) = Even(u) + Odd(u),  S(H - u) = Even(u) - Odd(u)   (cos(n (pi - x)) = (-1)^n cos(n x)),
+  // so lane slots cover u = 0..H/2 only; cos(n x) by the Chebyshev recurrence.
+  const int H = A.env_nfft >> 1;
+  double se[TS], so[TS], cprev[TS], ccur[TS], c2[TS];
 #pragma unroll
   for (int q = 0; q < TS; ++q) {
-    const int t = l + 16 * q;
-    const double c1 = A.env_cos[t % A.env_nfft];
-    sum[q] = cw[0];
+    const int u = l + 16 * q;
+    const double c1 = A.env_cos[u % A.env_nfft];
+    se[q] = cw[0];
+    so[q] = 0.0;
     cprev[q] = 1.0;
     ccur[q] = c1;
     c2[q] = 2.0 * c1;
   }
-  for (int n = 1; n < A.Me; ++n) {
-    const double w = cw[n];
+  int n = 1;
+  for (; n + 1 < A.Me; n += 2) {
+    const double wo = cw[n], we = cw[n + 1];
 #pragma unroll
     for (int q = 0; q < TS; ++q) {
-      sum[q] += w * ccur[q];
-      const double nxt = c2[q] * ccur[q] - cprev[q];
-      cprev[q] = ccur[q];
-      ccur[q] = nxt;
+      so[q] = fma(wo, ccur[q], so[q]);                  // odd n
+      const double c_e = fma(c2[q], ccur[q], -cprev[q]);
+      se[q] = fma(we, c_e, se[q]);                      // even n + 1
+      cprev[q] = c_e;
+      ccur[q] = fma(c2[q], c_e, -ccur[q]);
     }
   }
+  if (n < A.Me) {
+    const double wo = cw[n];
+#pragma unroll
+    for (int q = 0; q < TS; ++q) so[q] = fma(wo, ccur[q], so[q]);
+  }
   if (valid) {
+    double* out = A.env + (int64_t)item * A.kk;
 #pragma unroll
     for (int q = 0; q < TS; ++q) {
-      const int t = l + 16 * q;
-      if (t < A.kk) {
-        const double e = exp(sum[q]);
-        A.env[(int64_t)item * A.kk + t] = (e * A.env_win[2 * t]) / A.env_win[2 * t + 1];
-      }
+      const int u = l + 16 * q;
+      if (2 * u > H) continue;
+      if (u < A.kk) out[u] = (exp(se[q] + so[q]) * A.env_win[2 * u]) / A.env_win[2 * u + 1];
+      const int t2 = H - u;
+      if (t2 != u && t2 < A.kk) out[t2] = (exp(se[q] - so[q]) * A.env_win[2 * t2]) / A.env_win[2 * t2 + 1];
     }
   }
 }
@@ -1510,7 +1541,8 @@ static hipError_t launch_lpc_env_t(const LpcEnvArgs& A, size_t lds, hipStream_t 
 
 int lpc_env_region(int p, int M) {
   const int NAL = (M > p + 1 ? M : p + 1) + 16;
-  return NAL + (p + 2 > M ? p + 2 : M);
+  const int need = NAL + (p + 2 > M ? p + 2 : M);
+  return (need + 15) / 32 * 32 + 16;  // = 16 mod 32 doubles: the 4 items of a wave hit disjoint bank halves
 }
 
 hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int items, double* env,
@@ -1522,7 +1554,7 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
   A.r = r; A.weights = c.weights; A.env_cos = c.env_cos; A.env_win = c.env_win; A.env = env;
   A.a_out = a_out; A.gg_out = gg_out; A.cep_out = cep_out;
   const size_t lds = sizeof(double) * (4 * (size_t)A.region);
-  switch ((c.kk + 15) / 16) {
+  switch ((c.env_nfft / 4 + 1 + 15) / 16) {  // envelope slots: u = 0 .. env_nfft/4
 #define FDLP_TS_CASE(n) case n: return launch_lpc_env_t<n>(A, lds, s);
     FDLP_TS_CASE(1) FDLP_TS_CASE(2) FDLP_TS_CASE(3) FDLP_TS_CASE(4) FDLP_TS_CASE(5) FDLP_TS_CASE(6)
     FDLP_TS_CASE(7) FDLP_TS_CASE(8) FDLP_TS_CASE(9) FDLP_TS_CASE(10) FDLP_TS_CASE(11) FDLP_TS_CASE(12)
