@@ -53,8 +53,10 @@ struct DevConsts {
   const double* weights;   // [3, M] mask (:94-103), lifter (:195-196), gamma (:197-198); 1.0 if absent
   const double* env_cos;   // [env_nfft] cos(2*pi*q/env_nfft)
   const double* env_win;   // [kk, 2] (hanning(kk)[t], hamming(kk)[t]) interleaved (:205)
-  const double* tw1;       // [N1 * N2] four-step twiddles exp(-2*pi*i*n2*k1/N) (complex)
+  const double* tw1;       // [N1 * N2] four-step twiddles exp(-2*pi*i*n2*k1/(N1*N2)) (complex)
   const double* post;      // [N] complex exp(-i*pi*k/(2N)) (Makhoul post-twiddle)
+  const double* rtw;       // [N/2] complex exp(-2*pi*i*k/N) (real-FFT unpacking; real_fft only)
+  int real_fft;            // N even: the DCT runs a length-N/2 complex FFT of the packed real sequence
   // structured autocorrelation (cochlear filterbank, fixed skirt slope); null when not used
   const double* sk_e;      // [2, N] E = 10^(a (fw - c0)) (lower skirt), E' = 10^(-b (fw - c0)) (upper)
   const SkSnap* sk_snap;   // [2, B] sorted by S descending: S = N - m1_j (lower) / m2_j (upper) with

@@ -132,6 +132,44 @@ __device__ __forceinline__ int64_t reflect_idx(int64_t q, int64_t T) {
 
 __constant__ int kDiffTaps[13] = {1, 2, 3, 2, 0, -2, -5, -2, 0, 2, 3, 2, 1};  // :163
 
+// Windowed frame sample at Makhoul index n of v (v[n] = x[2n], v[N-1-n] = x[2n+1]).
+__device__ __forceinline__ double makhoul_sample(const DevConsts& c, const FrameDesc& fd, int n, int f,
+                                                 const void* __restrict__ pcm, int pcm_kind,
+                                                 const int16_t* __restrict__ noise,
+                                                 const double* __restrict__ dense_rows) {
+  const int N = c.N;
+  const int m = (2 * n < N) ? 2 * n : 2 * N - 1 - 2 * n;  // Makhoul even/odd split
+  if (dense_rows) return dense_rows[(int64_t)f * N + m];
+  const int64_t t = reflect_idx((int64_t)fd.k * c.hop + m - c.ext, fd.T);
+  double s;
+  if (pcm_kind == 0) {
+    s = (double)((const int16_t*)pcm)[fd.pcm_off + t];
+    if (fd.noise_off >= 0) {
+      // sig + alp*ns, evaluated in fp64 without contraction (features.py:31)
+      const double ns = (double)noise[fd.noise_off + t];
+      s = __dadd_rn(s, __dmul_rn(fd.alpha, ns));
+    }
+  } else if (pcm_kind == 1) {
+    s = ((const double*)pcm)[fd.pcm_off + t];
+  } else {
+    // pcm_kind 2: scipy.signal.convolve(int16 s, diff kernel, 'same') -> int64, exact
+    // (computeFDLPSpectrogram.py:162-164); 'same' = full[6 : 6+T], zeros outside [0, T)
+    const int16_t* x = (const int16_t*)pcm + fd.pcm_off;
+    long long acc = 0;
+#pragma unroll
+    for (int q = 0; q < 13; ++q) {
+      const int64_t idx = t + 6 - q;
+      if (idx >= 0 && idx < fd.T) acc += (long long)kDiffTaps[q] * (long long)x[idx];
+    }
+    s = (double)acc;
+  }
+  return __dmul_rn(s, c.hamming[m]);  // frame * win (features.py:153)
+}
+
+// REAL (even N): the real sequence v of length N is packed as z[q] = v[2q] + i v[2q+1] and
+// transformed with a length-N/2 complex FFT (dft2_dct_kernel<true> unpacks); otherwise v is
+// transformed as a complex sequence of length N.  The four-step split is N1 x N2 of that length.
+template <bool REAL>
 __global__ __launch_bounds__(256) void frames_dft1_kernel(
     DevConsts c, DftPlan d1, int N2, const void* __restrict__ pcm, int pcm_kind,
     const int16_t* __restrict__ noise, const FrameDesc* __restrict__ frames,
@@ -144,54 +182,30 @@ __global__ __launch_bounds__(256) void frames_dft1_kernel(
   double2* oms = smem + 2 * N1 * kDftCols;
   const int f = blockIdx.y;
   const int n2_0 = blockIdx.x * kDftCols;
-  const int N = c.N;
   for (int q = threadIdx.x; q < N1; q += blockDim.x) oms[q] = om1[q];
 
   FrameDesc fd;
   if (!dense_rows) fd = frames[f];
-  // load v[N2*n1 + n2] for n1 in [0,N1), n2 in [n2_0, n2_0+kDftCols)
+  // load z[N2*n1 + n2] for n1 in [0,N1), n2 in [n2_0, n2_0+kDftCols)
   for (int e = threadIdx.x; e < N1 * kDftCols; e += blockDim.x) {
     const int col = e % kDftCols;
     const int n1 = e / kDftCols;
     const int n2 = n2_0 + col;
-    double val = 0.0;
+    double2 val = make_double2(0.0, 0.0);
     if (n2 < N2) {
-      const int n = N2 * n1 + n2;
-      const int m = (2 * n < N) ? 2 * n : 2 * N - 1 - 2 * n;  // Makhoul even/odd split
-      if (dense_rows) {
-        val = dense_rows[(int64_t)f * N + m];
+      const int q = N2 * n1 + n2;
+      if constexpr (REAL) {
+        val.x = makhoul_sample(c, fd, 2 * q, f, pcm, pcm_kind, noise, dense_rows);
+        val.y = makhoul_sample(c, fd, 2 * q + 1, f, pcm, pcm_kind, noise, dense_rows);
       } else {
-        const int64_t t = reflect_idx((int64_t)fd.k * c.hop + m - c.ext, fd.T);
-        double s;
-        if (pcm_kind == 0) {
-          s = (double)((const int16_t*)pcm)[fd.pcm_off + t];
-          if (fd.noise_off >= 0) {
-            // sig + alp*ns, evaluated in fp64 without contraction (features.py:31)
-            const double ns = (double)noise[fd.noise_off + t];
-            s = __dadd_rn(s, __dmul_rn(fd.alpha, ns));
-          }
-        } else if (pcm_kind == 1) {
-          s = ((const double*)pcm)[fd.pcm_off + t];
-        } else {
-          // pcm_kind 2: scipy.signal.convolve(int16 s, diff kernel, 'same') -> int64, exact
-          // (computeFDLPSpectrogram.py:162-164); 'same' = full[6 : 6+T], zeros outside [0, T)
-          const int16_t* x = (const int16_t*)pcm + fd.pcm_off;
-          long long acc = 0;
-#pragma unroll
-          for (int q = 0; q < 13; ++q) {
-            const int64_t idx = t + 6 - q;
-            if (idx >= 0 && idx < fd.T) acc += (long long)kDiffTaps[q] * (long long)x[idx];
-          }
-          s = (double)acc;
-        }
-        val = __dmul_rn(s, c.hamming[m]);  // frame * win (features.py:153)
+        val.x = makhoul_sample(c, fd, q, f, pcm, pcm_kind, noise, dense_rows);
       }
     }
-    bufA[n1 * kDftCols + col] = make_double2(val, 0.0);
+    bufA[n1 * kDftCols + col] = val;
   }
   __syncthreads();
   double2* res = lds_dft(bufA, bufB, oms, d1, kDftCols);
-  // twiddle exp(-2 pi i n2 k1 / N) and store z[f][k1][n2]
+  // twiddle exp(-2 pi i n2 k1 / (N1 N2)) and store z[f][k1][n2]
   for (int e = threadIdx.x; e < N1 * kDftCols; e += blockDim.x) {
     const int col = e % kDftCols;
     const int k1 = e / kDftCols;
@@ -205,7 +219,11 @@ __global__ __launch_bounds__(256) void frames_dft1_kernel(
 
 // -----------------------------------------------------------------------------------------
 // 2. row DFTs (length N2) + Makhoul post-twiddle -> DCT-II / sqrt(2N)
+//    REAL: Z = FFT_{N/2}(z) is unpacked into V = FFT_N(v) with E = (Z_k + conj Z_{M-k})/2,
+//    O = (Z_k - conj Z_{M-k})/(2i), V_k = E + w^k O, V_{k+M} = E - w^k O (w = e^{-2 pi i/N},
+//    M = N/2).  A workgroup holds rows k1 and N1-k1 (4 such pairs), so Z_{M-k} is in its LDS.
 // -----------------------------------------------------------------------------------------
+template <bool REAL>
 __global__ __launch_bounds__(256) void dft2_dct_kernel(DevConsts c, DftPlan d2, int N1,
                                                        const double2* __restrict__ z,
                                                        const double2* __restrict__ om2,
@@ -216,27 +234,57 @@ __global__ __launch_bounds__(256) void dft2_dct_kernel(DevConsts c, DftPlan d2, 
   double2* bufB = smem + N2 * kDftCols;
   double2* oms = smem + 2 * N2 * kDftCols;
   const int f = blockIdx.y;
-  const int k1_0 = blockIdx.x * kDftCols;
   const int N = c.N;
+  constexpr int kHalf = kDftCols / 2;
+  // slot -> row k1 (-1: unused).  REAL: slots r and r + 4 hold the rows of pair pp = 4 b + r,
+  // (pp, N1 - pp); a self-paired row (pp = 0 or 2 pp = N1) occupies slot r only.
+  auto slot_row = [&](int r) -> int {
+    if constexpr (REAL) {
+      const int pp = blockIdx.x * kHalf + (r % kHalf);
+      if (2 * pp > N1) return -1;
+      if (r < kHalf) return pp;
+      const int m = N1 - pp;
+      return (pp == 0 || m == pp) ? -1 : m;
+    } else {
+      const int k1 = blockIdx.x * kDftCols + r;
+      return k1 < N1 ? k1 : -1;
+    }
+  };
   for (int q = threadIdx.x; q < N2; q += blockDim.x) oms[q] = om2[q];
   for (int e = threadIdx.x; e < N2 * kDftCols; e += blockDim.x) {
     const int row = e / N2;  // coalesced over n2
     const int n2 = e % N2;
-    const int k1 = k1_0 + row;
+    const int k1 = slot_row(row);
     double2 v = make_double2(0.0, 0.0);
-    if (k1 < N1) v = z[((int64_t)f * N1 + k1) * N2 + n2];
+    if (k1 >= 0) v = z[((int64_t)f * N1 + k1) * N2 + n2];
     bufA[n2 * kDftCols + row] = v;
   }
   __syncthreads();
   double2* res = lds_dft(bufA, bufB, oms, d2, kDftCols);
+  const double2* post = (const double2*)c.post;
   for (int e = threadIdx.x; e < N2 * kDftCols; e += blockDim.x) {
     const int row = e % kDftCols;
     const int k2 = e / kDftCols;
-    const int k1 = k1_0 + row;
-    if (k1 < N1) {
-      const int k = k1 + N1 * k2;
-      const double2 V = res[k2 * kDftCols + row];
-      const double2 w = ((const double2*)c.post)[k];
+    const int k1 = slot_row(row);
+    if (k1 < 0) continue;
+    const int k = k1 + N1 * k2;
+    const double2 V = res[k2 * kDftCols + row];
+    if constexpr (REAL) {
+      const int M = N1 * N2;
+      const int km = k == 0 ? 0 : M - k;  // Z_M = Z_0
+      const int k1m = km % N1, k2m = km / N1;
+      const int rm = k1m == k1 ? row : (row < kHalf ? row + kHalf : row - kHalf);
+      const double2 W = res[k2m * kDftCols + rm];
+      const double2 E = make_double2(0.5 * (V.x + W.x), 0.5 * (V.y - W.y));
+      const double2 O = make_double2(0.5 * (V.y + W.y), -0.5 * (V.x - W.x));
+      const double2 t = cmul(((const double2*)c.rtw)[k], O);
+      const double2 V1 = make_double2(E.x + t.x, E.y + t.y);
+      const double2 V2 = make_double2(E.x - t.x, E.y - t.y);
+      const double2 w1 = post[k], w2 = post[k + M];
+      dct[(int64_t)f * N + k] = 2.0 * (w1.x * V1.x - w1.y * V1.y) / inv_scale_div;
+      dct[(int64_t)f * N + k + M] = 2.0 * (w2.x * V2.x - w2.y * V2.y) / inv_scale_div;
+    } else {
+      const double2 w = post[k];
       const double y = 2.0 * (w.x * V.x - w.y * V.y);
       dct[(int64_t)f * N + k] = y / inv_scale_div;  // dct(.)/np.sqrt(2N)  (:178)
     }
@@ -1376,20 +1424,32 @@ hipError_t launch_frames_dft1(const DevConsts& c, const DftPlan& d1, int N2, con
   if (nframes <= 0) return hipSuccess;
   dim3 grid((N2 + kDftCols - 1) / kDftCols, nframes);
   size_t lds = sizeof(double2) * (2 * d1.n * kDftCols + d1.n);
-  if (lds > 65536) (void)hipFuncSetAttribute((const void*)frames_dft1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(frames_dft1_kernel, grid, dim3(256), lds, s, c, d1, N2, pcm, pcm_kind, noise,
-                     frames, dense_rows, om1, z);
+  if (c.real_fft) {
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)frames_dft1_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(frames_dft1_kernel<true>, grid, dim3(256), lds, s, c, d1, N2, pcm, pcm_kind, noise,
+                       frames, dense_rows, om1, z);
+  } else {
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)frames_dft1_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(frames_dft1_kernel<false>, grid, dim3(256), lds, s, c, d1, N2, pcm, pcm_kind, noise,
+                       frames, dense_rows, om1, z);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const double2* z,
                            int nframes, double* dct, const double2* om2, hipStream_t s) {
   if (nframes <= 0) return hipSuccess;
-  dim3 grid((N1 + kDftCols - 1) / kDftCols, nframes);
   size_t lds = sizeof(double2) * (2 * d2.n * kDftCols + d2.n);
-  if (lds > 65536) (void)hipFuncSetAttribute((const void*)dft2_dct_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const double div = sqrt((double)(2 * c.N));
-  hipLaunchKernelGGL(dft2_dct_kernel, grid, dim3(256), lds, s, c, d2, N1, z, om2, div, dct);
+  if (c.real_fft) {
+    dim3 grid((N1 / 2 + 1 + kDftCols / 2 - 1) / (kDftCols / 2), nframes);  // row pairs (k1, N1-k1)
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)dft2_dct_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(dft2_dct_kernel<true>, grid, dim3(256), lds, s, c, d2, N1, z, om2, div, dct);
+  } else {
+    dim3 grid((N1 + kDftCols - 1) / kDftCols, nframes);
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)dft2_dct_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(dft2_dct_kernel<false>, grid, dim3(256), lds, s, c, d2, N1, z, om2, div, dct);
+  }
   return hipGetLastError();
 }
 

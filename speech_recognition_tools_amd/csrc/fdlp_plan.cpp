@@ -223,6 +223,8 @@ struct fdlp_plan {
   // geometry (computeFDLPSpectrogram.py / features.py float expressions)
   int N = 0, nfft = 0, hop = 0, sp_b = 0, sp_f = 0, ext = 0, env_nfft = 0, kk = 0, kkb2 = 0, ola_hop = 0;
   int B = 0, p = 0, M = 0, nlags = 0, Me = 0, ncol = 0;
+  bool real_fft = false;  // even N: packed length-N/2 complex FFT
+  int nfft_c = 0;         // complex FFT length N1 * N2 (N/2 or N)
   fdlp::DftPlan d1{}, d2{};
   std::vector<double> fbank_host;  // [B, ncol]
   std::vector<int> lo, hi;
@@ -230,7 +232,7 @@ struct fdlp_plan {
   // device constants
   fdlp::DevConsts dc{};
   double *d_fbank = nullptr, *d_hamming = nullptr, *d_weights = nullptr, *d_env_cos = nullptr,
-         *d_env_win = nullptr, *d_tw1 = nullptr, *d_post = nullptr;
+         *d_env_win = nullptr, *d_tw1 = nullptr, *d_post = nullptr, *d_rtw = nullptr;
   double2 *d_om1 = nullptr, *d_om2 = nullptr;
   int *d_lo = nullptr, *d_hi = nullptr;
   // workspace
@@ -288,7 +290,7 @@ int free_plan(fdlp_plan* p) {
   if (!p) return FDLP_OK;
   for (auto& ev : p->prof_pending)
     for (auto e : ev) (void)hipEventDestroy(e);
-  void* devs[] = {p->d_fbank, p->d_hamming, p->d_weights, p->d_env_cos, p->d_env_win, p->d_tw1, p->d_post,
+  void* devs[] = {p->d_fbank, p->d_hamming, p->d_weights, p->d_env_cos, p->d_env_win, p->d_tw1, p->d_post, p->d_rtw,
                   p->d_om1, p->d_om2, p->d_lo, p->d_hi, p->ws.z, p->ws.dct, p->ws.r, p->ws.a, p->ws.gg,
                   p->ws.cep, p->ws.env, p->d_frames, p->d_utts, p->d_sk_e, p->r_up, p->d_sk_snap,
                   p->d_sk_reg};
@@ -405,7 +407,9 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   if ((p->p + 1 + 15) / 16 > 15) PLAN_FAIL(FDLP_E_INVALID, "order too large for the Levinson kernel");
   if (p->kk > 256) PLAN_FAIL(FDLP_E_INVALID, "fduration*frate too large (envelope > 256 samples)");
   if (p->M > 4096) PLAN_FAIL(FDLP_E_INVALID, "coeff_num too large (max 4096)");
-  if (!split_four_step(p->N, &p->d1, &p->d2))
+  p->real_fft = p->N % 2 == 0 && split_four_step(p->N / 2, &p->d1, &p->d2);
+  p->nfft_c = p->real_fft ? p->N / 2 : p->N;  // complex FFT length of the DCT
+  if (!p->real_fft && !split_four_step(p->nfft_c, &p->d1, &p->d2))
     PLAN_FAIL(FDLP_E_INVALID, "frame length int(srate*fduration) has no supported 2/3/5/7 four-step split");
 
   // filterbank (:49-63)
@@ -467,16 +471,21 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   std::vector<double> env_cos(p->env_nfft);
   for (int q = 0; q < p->env_nfft; ++q)
     env_cos[q] = (double)cosl(2.0L * (long double)M_PI * (long double)q / (long double)p->env_nfft);
-  const int N1 = p->d1.n, N2 = p->d2.n, N = p->N;
-  std::vector<double> tw1(2 * (size_t)N1 * N2), post(2 * (size_t)N);
+  const int N1 = p->d1.n, N2 = p->d2.n, N = p->N, NC = p->nfft_c;
+  std::vector<double> tw1(2 * (size_t)N1 * N2), post(2 * (size_t)N), rtw(2 * (size_t)std::max(1, N / 2));
   const long double PI = 3.141592653589793238462643383279502884L;
   for (int k1 = 0; k1 < N1; ++k1)
     for (int n2 = 0; n2 < N2; ++n2) {
-      const long long q = ((long long)k1 * n2) % N;
-      const long double ang = -2.0L * PI * (long double)q / (long double)N;
+      const long long q = ((long long)k1 * n2) % NC;
+      const long double ang = -2.0L * PI * (long double)q / (long double)NC;
       tw1[2 * ((size_t)k1 * N2 + n2)] = (double)cosl(ang);
       tw1[2 * ((size_t)k1 * N2 + n2) + 1] = (double)sinl(ang);
     }
+  for (int k = 0; k < N / 2; ++k) {
+    const long double ang = -2.0L * PI * (long double)k / (long double)N;
+    rtw[2 * k] = (double)cosl(ang);
+    rtw[2 * k + 1] = (double)sinl(ang);
+  }
   for (int k = 0; k < N; ++k) {
     const long double ang = -PI * (long double)k / (2.0L * (long double)N);
     post[2 * k] = (double)cosl(ang);
@@ -512,6 +521,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   PLAN_TRY(upload(&p->d_env_win, env_win.data(), env_win.size()));
   PLAN_TRY(upload(&p->d_tw1, tw1.data(), tw1.size()));
   PLAN_TRY(upload(&p->d_post, post.data(), post.size()));
+  PLAN_TRY(upload(&p->d_rtw, rtw.data(), rtw.size()));
   PLAN_TRY(upload(&p->d_om1, om1.data(), om1.size()));
   PLAN_TRY(upload(&p->d_om2, om2.data(), om2.size()));
 
@@ -520,6 +530,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   d.kk = p->kk; d.env_nfft = p->env_nfft;
   d.fbank = p->d_fbank; d.lo = p->d_lo; d.hi = p->d_hi; d.hamming = p->d_hamming; d.weights = p->d_weights;
   d.env_cos = p->d_env_cos; d.env_win = p->d_env_win; d.tw1 = p->d_tw1; d.post = p->d_post;
+  d.rtw = p->d_rtw; d.real_fft = p->real_fft ? 1 : 0;
   if (p->sk_avail) {
     PLAN_TRY(upload(&p->d_sk_e, p->sk.e.data(), p->sk.e.size()));
     PLAN_TRY(upload(&p->d_sk_snap, p->sk.snap.data(), p->sk.snap.size()));
@@ -531,7 +542,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   // workspace
   const size_t F = (size_t)c.max_frames, items = F * p->B;
   p->max_frames = c.max_frames;
-  if (hipMalloc((void**)&p->ws.z, sizeof(double2) * F * N) != hipSuccess ||
+  if (hipMalloc((void**)&p->ws.z, sizeof(double2) * F * p->nfft_c) != hipSuccess ||
       hipMalloc((void**)&p->ws.dct, sizeof(double) * F * N) != hipSuccess ||
       hipMalloc((void**)&p->ws.r, sizeof(double) * items * p->nlags) != hipSuccess ||
       hipMalloc((void**)&p->ws.a, sizeof(double) * items * (p->p + 1)) != hipSuccess ||
@@ -703,9 +714,9 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     HIP_TRY(mark(0));
     HIP_TRY(fdlp::launch_frames_dft1(p->dc, p->d1, p->d2.n, b->pcm_dev,
                                      b->preprocess == FDLP_PRE_DIFF ? 2 : b->pcm_kind, b->noise_dev, p->d_frames + f0,
-                                     nullptr, n, p->ws.z + f0 * N, p->d_om1, st));
+                                     nullptr, n, p->ws.z + f0 * p->nfft_c, p->d_om1, st));
     HIP_TRY(mark(1));
-    HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z + f0 * N, n, p->ws.dct + f0 * N, p->d_om2, st));
+    HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z + f0 * p->nfft_c, n, p->ws.dct + f0 * N, p->d_om2, st));
     HIP_TRY(mark(2));
     if (p->ac_path == FDLP_AC_STRUCTURED) {
       HIP_TRY(fdlp::launch_autocorr_structured(p->dc, p->ws.dct + f0 * N, n, r, p->r_up + it0 * nl, st));

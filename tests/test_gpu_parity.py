@@ -198,3 +198,19 @@ def test_pipelined_sub_batches_match_serial():
         res.append(out64.cpu().numpy())
     np.testing.assert_array_equal(res[0], res[1])
     np.testing.assert_array_equal(res[0], res[2])
+
+
+@pytest.mark.parametrize("fduration", [0.5, 0.5315625, 1.5])
+def test_dct_rows_even_and_odd_lengths(fduration):
+    """fdlp_dct_rows == scipy dct-II / sqrt(2N) (computeFDLPSpectrogram.py:178) for an even N
+    (packed half-length FFT: 8000, 24000) and an odd N (full-length complex FFT: 8505)."""
+    import scipy.fft
+    from speech_recognition_tools_amd import FdlpPlan, FeatureConfig
+    cfg = FeatureConfig(fduration=fduration, nfilters=20, order=30, coeff_num=30, coeff_range="0,30")
+    plan = FdlpPlan(cfg, device=0, max_frames=8)
+    N = plan.N
+    rng = np.random.default_rng(N)
+    x = rng.standard_normal((5, N)) * np.linspace(1, 100, N)
+    y = plan.dct_rows(torch.from_numpy(x).cuda()).cpu().numpy()
+    ref = scipy.fft.dct(x, type=2, axis=-1) / np.sqrt(2 * N)
+    assert np.abs(y - ref).max() <= 1e-12 * np.abs(ref).max()
