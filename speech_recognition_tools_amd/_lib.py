@@ -107,7 +107,7 @@ class FdlpError(RuntimeError):
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError("libfdlp_hip.so not built (%s); run __graft_entry__.build() or "
-                          "python -m speech_recognition_tools_amd._build" % LIB_PATH)
+                          "python speech_recognition_tools_amd/_build.py" % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
