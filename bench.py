@@ -68,7 +68,14 @@ def cpu_baseline(cfg_name, T, workers, per_worker):
                        (workers * per_worker, T / 16000.0, per_worker))
 
 
-PMC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc.json")
+def _latest_pmc():
+    """The newest committed PMC summary (profiles/rNN*_pmc.json, written by scripts/round_evidence.sh)."""
+    import glob
+    c = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc.json")))
+    return c[-1] if c else None
+
+
+PMC_FILE = _latest_pmc()
 AC_KERNEL_PREFIX = {"structured": ("fdlp::ac_sweep_kernel", "fdlp::ac_band_kernel"),
                     "direct": ("fdlp::autocorr_kernel",)}
 
@@ -79,7 +86,7 @@ def stage_traffic(path):
     (gfx950 correction, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, KiB -> bytes.  None if absent."""
     try:
         rows = json.load(open(PMC_FILE))
-    except (OSError, ValueError):
+    except (OSError, ValueError, TypeError):
         return None
     tot, seen = 0.0, 0
     for name, m in rows.items():
@@ -139,7 +146,8 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from speech_recognition_tools_amd import FdlpPlan, FeatureConfig, PyRandom, DEFAULT_SUPPORT_EPS
+    from speech_recognition_tools_amd import FdlpPlan, FeatureConfig, PyRandom
+    from speech_recognition_tools_amd.shard import timed_steps
 
     if world > 1:
         torch.cuda.set_device(local)
@@ -169,25 +177,10 @@ def main():
     def step():
         plan.compute(pcm, lens, rng.randbits2(nj), out=out)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    plan.set_profiling(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    # warmup, barrier + sync, exactly K steps, sync + barrier, max over ranks (speech_recognition_tools_amd.shard)
+    elapsed = timed_steps(step, args.steps, args.warmup, lambda: torch.cuda.synchronize(dev),
+                          dist if world > 1 else None, dev, before_timed=lambda: plan.set_profiling(True))
     stages, ncalls = plan.stage_times()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     audio_h = world * args.steps * args.utts * T / 16000.0 / 3600.0
     value = audio_h / elapsed
@@ -217,7 +210,7 @@ def main():
         "roofline": {"bound": "mfma", "kernel": AC_KERNELS[plan.autocorr_path],
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": stage_traffic(plan.autocorr_path),
-                     "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/r01_pmc.json)",
+                     "traffic_unit": "bytes/launch (rocprofv3 PMC, %s)" % os.path.relpath(PMC_FILE or "none", ROOT),
                      "avg_launch_ms": ac_ms, "algorithmic_flops_per_launch": flops_per_launch},
         "stage_ms_per_step": {k: v / max(ncalls, 1) for k, v in stages.items()},
         "cpu_baseline": cpu,

@@ -76,19 +76,7 @@ $write_utt2num_frames && add_opts="$add_opts --write_utt2num_frames"
 split_list() {  # split_list <in> <out1> ... : contiguous, balanced, like utils/split_scp.pl
   local in=$1; shift
   if [ -f utils/split_scp.pl ]; then utils/split_scp.pl "$in" "$@"; return $?; fi
-  python3 - "$in" "$@" <<'PY'
-import sys
-lines = open(sys.argv[1]).read().splitlines(True)
-outs = sys.argv[2:]
-n, k = len(lines), len(outs)
-if n < k:
-    sys.exit("split_scp: fewer lines (%d) than jobs (%d)" % (n, k))
-pos = 0
-for i, o in enumerate(outs):
-    m = n // k + (1 if i < n % k else 0)
-    open(o, "w").writelines(lines[pos:pos + m])
-    pos += m
-PY
+  python3 "$here/speech_recognition_tools_amd/shard.py" "$in" "$@"
 }
 
 run_jobs() {  # run_jobs <list-pattern containing JOB> <scp-type-opt>
