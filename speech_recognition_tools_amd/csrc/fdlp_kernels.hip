@@ -21,6 +21,8 @@
 //   7. ola_log      : deterministic gather OLA + floor + log -> float32 [L, B].  (:207-229)
 #include <hip/hip_runtime.h>
 #include <math.h>
+
+#include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -1278,6 +1280,187 @@ __device__ __forceinline__ void cep_block_step(int b0, int M, int l, double gg, 
   if constexpr (KK + 1 < 16) cep_block_step<KK + 1>(b0, M, l, gg, inv_n, la, n, acc, mine);
 }
 
+#ifndef FDLP_LPC_PHASES
+#define FDLP_LPC_PHASES 7  // bit 0 Durbin, 1 cepstrum, 2 envelope (benchmarks/lpc_env_phases.hip only)
+#endif
+
+// -----------------------------------------------------------------------------------------
+// Durbin in lattice form, register-resident (no LDS traffic, no barriers).  Lane l of the 16-lane
+// row owns positions m = l + 16 s (s < SL) of
+//   A = a^(k)   (a_0 = 1)                      and   B = the reversed predictor, b_m = a_{k-1-m},
+//   R1[m] = r_{m+1},
+// so the order-k dot product  r_k + sum_{i=1}^{k-1} a_i r_{k-i} = sum_{m<k} b_m r_{m+1}  is lane-aligned,
+// and the update  a_i <- a_i + kappa a_{k-i}  is  A <- A + kappa (z B),  B <- (z B) + kappa A  with z the
+// shift by one position (DPP row_ror:1, lane 0 takes lane 15 of the previous slot).  This is the same
+// arithmetic as the reference's recursion (features.py:226-228 via solve_toeplitz): fma(kappa, a_{k-i}, a_i)
+// for both halves of every symmetric pair, so B stays the bitwise mirror of A.  Orders k in
+// [16Q, 16Q+16) touch slots 0..Q only (positions > k are zero), hence the per-phase templates.
+// -----------------------------------------------------------------------------------------
+template <int SL, int Q>
+__device__ __forceinline__ void lattice_phase(double (&A)[SL], double (&B)[SL], const double (&R1)[SL], double& E,
+                                              int k0, int k1, bool lane0) {
+  for (int k = k0; k < k1; ++k) {
+    double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+    for (int s = 0; s <= Q; s += 2) p0 = fma(B[s], R1[s], p0);
+#pragma unroll
+    for (int s = 1; s <= Q; s += 2) p1 = fma(B[s], R1[s], p1);
+    const double acc = row_sum16(p0 + p1);
+    double rE = __builtin_amdgcn_rcp(E);
+    rE = fma(rE, fma(-E, rE, 1.0), rE);
+    rE = fma(rE, fma(-E, rE, 1.0), rE);
+    const double kappa = -acc * rE;
+    double rot[Q + 1];
+#pragma unroll
+    for (int s = 0; s <= Q; ++s) rot[s] = dpp_f64<0x121>(B[s]);  // row_ror:1
+#pragma unroll
+    for (int s = 0; s <= Q; ++s) {
+      // B first: its old value lives on in rot[], so both updates are in place (no register copies)
+      const double bsh = lane0 ? (s == 0 ? 0.0 : rot[s - 1]) : rot[s];
+      B[s] = fma(kappa, A[s], bsh);
+      A[s] = fma(kappa, bsh, A[s]);
+    }
+    E = E * (1.0 - kappa * kappa);
+  }
+}
+
+template <int SL, int Q>
+__device__ __forceinline__ void lattice_durbin(double (&A)[SL], double (&B)[SL], const double (&R1)[SL], double& E,
+                                               int p, bool lane0) {
+  const int k0 = Q == 0 ? 1 : 16 * Q;
+  const int k1 = min(p + 1, 16 * Q + 16);
+  if (k0 < k1) lattice_phase<SL, Q>(A, B, R1, E, k0, k1, lane0);
+  if constexpr (Q + 1 < SL) lattice_durbin<SL, Q + 1>(A, B, R1, E, p, lane0);
+}
+
+// lpc_env with the lattice Durbin: persistent waves (grid-stride over groups of 4 items), r read
+// straight into registers, LDS only for a (cepstrum) and c (envelope).  Same outputs as lpc_env_kernel.
+constexpr int kEnvChunk = 5;  // envelope slots held in registers at a time
+template <int SL>
+__global__ __launch_bounds__(64, 4) void lpc_env_lattice_kernel(LpcEnvArgs A_) {
+  extern __shared__ double sh[];
+  const LpcEnvArgs& A = A_;
+  const int ngroups = (A.items + 3) >> 2;
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    // Everything below is re-derived per group from opaque copies, so the compiler cannot hoist
+    // group-invariant addresses/tables out of the loop (they would stay live through the Durbin phase).
+    int tid = threadIdx.x, p = A.p, M = A.M;
+    asm volatile("" : "+v"(tid));
+    asm volatile("" : "+s"(p), "+s"(M));
+    const int g = tid >> 4;
+    const int l = tid & 15;
+    const bool lane0 = l == 0;
+    const int nlags = A.nlags;
+    const int NAL = (M > p + 1 ? M : p + 1) + 16;
+    double* la = sh + g * A.region;  // a_0..a_p, zeros up to NAL
+    double* cs = la + NAL;           // c_0..c_{M-1}
+    const int H = A.env_nfft >> 1;
+    const int TS = (A.env_nfft / 4 + 1 + 15) / 16;
+    const int item = grp * 4 + g;
+    const bool valid = item < A.items;
+    // ---- phase 1: Levinson-Durbin (features.py:226-228) in registers -------------------------
+    double Av[SL], Bv[SL], R1[SL];
+    const double* rr = A.r + (int64_t)(valid ? item : 0) * nlags;
+#pragma unroll
+    for (int s = 0; s < SL; ++s) {  // branch-free: clamped loads, then select
+      const int m = l + 16 * s;
+      const double v = rr[min(m + 1, nlags - 1)];
+      R1[s] = (valid && m <= p) ? v : 0.0;
+      Av[s] = (m == 0) ? 1.0 : 0.0;
+      Bv[s] = Av[s];
+    }
+    const double r0v = rr[0];
+    const double r0 = valid ? r0v : 1.0;
+    double E = r0;
+    if (FDLP_LPC_PHASES & 1) lattice_durbin<SL, 0>(Av, Bv, R1, E, p, lane0);
+    double part = 0.0;
+#pragma unroll
+    for (int s = 0; s < SL; ++s) part = fma(Av[s], R1[s], part);
+    const double gg = r0 + row_sum16(part);  // the reference's off-by-one gain (features.py:228)
+    wave_lds_sync();  // the previous group's envelope reads of la are done
+#pragma unroll
+    for (int s = 0; s < SL; ++s) {
+      const int m = l + 16 * s;
+      if (m < NAL) la[m] = m <= p ? Av[s] : 0.0;
+      if (valid && A.a_out && m <= p) A.a_out[(int64_t)item * (p + 1) + m] = Av[s];
+    }
+    for (int q = l + 16 * SL; q < NAL; q += 16) la[q] = 0.0;
+    if (valid && A.a_out && lane0) A.gg_out[item] = gg;
+    wave_lds_sync();
+    // ---- phase 2: cepstrum (features.py:233-246), as in lpc_env_kernel -------------------------
+    for (int b0 = 0; b0 < ((FDLP_LPC_PHASES & 2) ? M : 0); b0 += 16) {
+      const int n = b0 + l;
+      const double inv_n = 1.0 / (double)(n > 0 ? n : 1);
+      double acc = 0.0;
+      const int kstart = max(1, b0 - p);
+      double kd = (double)kstart;
+      for (int k = kstart; k < b0; ++k, kd += 1.0) acc = fma(kd * cs[k], la[n - k], acc);
+      double mine = 0.0;
+      cep_block_step<0>(b0, M, l, gg, inv_n, la, n, acc, mine);
+      if (n < M) {
+        cs[n] = mine;
+        if (valid && A.cep_out) A.cep_out[(int64_t)item * M + n] = mine;
+      }
+      wave_lds_sync();
+    }
+    // ---- phase 3: weights + envelope (computeFDLPSpectrogram.py:194-205) ---------------------
+    double* cw = la;
+    const double* mask = A.weights;
+    const double* lif = A.weights + M;
+    const double* gam = A.weights + 2 * M;
+    for (int n = l; n < A.Me; n += 16) {
+      double v = cs[n];
+      v = v * mask[n];
+      v = v * lif[n];
+      v = v * gam[n];
+      if (A.odd_zero && (n & 1)) v = 0.0;
+      cw[n] = v;
+    }
+    wave_lds_sync();
+    // S(u) = Even(u) + Odd(u), S(H - u) = Even(u) - Odd(u); lane slots cover u = 0..H/2 (lpc_env_kernel)
+    for (int q0 = 0; q0 < TS; q0 += kEnvChunk) {
+      double se[kEnvChunk], so[kEnvChunk], cprev[kEnvChunk], ccur[kEnvChunk], c2[kEnvChunk];
+#pragma unroll
+      for (int q = 0; q < kEnvChunk; ++q) {
+        const int u = l + 16 * (q0 + q);
+        const double c1 = A.env_cos[u % A.env_nfft];
+        se[q] = cw[0];
+        so[q] = 0.0;
+        cprev[q] = 1.0;
+        ccur[q] = c1;
+        c2[q] = 2.0 * c1;
+      }
+      int n = 1;
+      for (; n + 1 < ((FDLP_LPC_PHASES & 4) ? A.Me : 0); n += 2) {
+        const double wo = cw[n], we = cw[n + 1];
+#pragma unroll
+        for (int q = 0; q < kEnvChunk; ++q) {
+          so[q] = fma(wo, ccur[q], so[q]);
+          const double c_e = fma(c2[q], ccur[q], -cprev[q]);
+          se[q] = fma(we, c_e, se[q]);
+          cprev[q] = c_e;
+          ccur[q] = fma(c2[q], c_e, -ccur[q]);
+        }
+      }
+      if (n < A.Me) {
+        const double wo = cw[n];
+#pragma unroll
+        for (int q = 0; q < kEnvChunk; ++q) so[q] = fma(wo, ccur[q], so[q]);
+      }
+      if (valid) {
+        double* out = A.env + (int64_t)item * A.kk;
+#pragma unroll
+        for (int q = 0; q < kEnvChunk; ++q) {
+          const int u = l + 16 * (q0 + q);
+          if (2 * u > H) continue;
+          if (u < A.kk) out[u] = (exp(se[q] + so[q]) * A.env_win[2 * u]) / A.env_win[2 * u + 1];
+          const int t2 = H - u;
+          if (t2 != u && t2 < A.kk) out[t2] = (exp(se[q] - so[q]) * A.env_win[2 * t2]) / A.env_win[2 * t2 + 1];
+        }
+      }
+    }
+  }
+}
 template <int TS>
 __global__ __launch_bounds__(64) void lpc_env_kernel(LpcEnvArgs A) {
   extern __shared__ double sh[];
@@ -1293,7 +1476,7 @@ __global__ __launch_bounds__(64) void lpc_env_kernel(LpcEnvArgs A) {
   for (int q = l; q < nlags; q += 16) lr[q] = valid ? A.r[(int64_t)item * nlags + q] : 1.0;
   for (int q = l; q < NAL; q += 16) la[q] = q == 0 ? 1.0 : 0.0;
   wave_lds_sync();
-  const double gg = durbin16(la, lr, p, l);
+  const double gg = (FDLP_LPC_PHASES & 1) ? durbin16(la, lr, p, l) : lr[0];
   if (valid && A.a_out) {
     for (int i = l; i <= p; i += 16) A.a_out[(int64_t)item * (p + 1) + i] = la[i];
     if (l == 0) A.gg_out[item] = gg;
@@ -1303,7 +1486,7 @@ __global__ __launch_bounds__(64) void lpc_env_kernel(LpcEnvArgs A) {
   // blocks of 16 coefficients: the finished blocks enter as a lane-parallel dot product, the block
   // itself as a 16-step recurrence with the new c_k broadcast along the row.
   double* cs = lr;
-  for (int b0 = 0; b0 < M; b0 += 16) {
+  for (int b0 = 0; b0 < ((FDLP_LPC_PHASES & 2) ? M : 0); b0 += 16) {
     const int n = b0 + l;
     const double inv_n = 1.0 / (double)(n > 0 ? n : 1);
     double acc = 0.0;
@@ -1348,7 +1531,7 @@ __global__ __launch_bounds__(64) void lpc_env_kernel(LpcEnvArgs A) {
     c2[q] = 2.0 * c1;
   }
   int n = 1;
-  for (; n + 1 < A.Me; n += 2) {
+  for (; n + 1 < ((FDLP_LPC_PHASES & 4) ? A.Me : 0); n += 2) {
     const double wo = cw[n], we = cw[n + 1];
 #pragma unroll
     for (int q = 0; q < TS; ++q) {
@@ -1605,6 +1788,28 @@ int lpc_env_region(int p, int M) {
   return (need + 15) / 32 * 32 + 16;  // = 16 mod 32 doubles: the 4 items of a wave hit disjoint bank halves
 }
 
+template <int SL>
+static hipError_t launch_lpc_lattice_sl(const LpcEnvArgs& A, size_t lds, hipStream_t s) {
+  static int per_cu = -1, cus = 0;  // resident waves per CU at this LDS size (one wave per block)
+  static size_t per_cu_lds = 0;
+  if (per_cu < 0 || per_cu_lds != lds) {
+    if (lds > 65536)
+      (void)hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lpc_env_lattice_kernel<SL>, 64, lds) != hipSuccess || n < 1)
+      n = 4;
+    per_cu = n;
+    per_cu_lds = lds;
+  }
+  const int groups = (A.items + 3) / 4;
+  const int grid = std::min(groups, std::max(1, per_cu * std::max(cus, 1)));
+  hipLaunchKernelGGL((lpc_env_lattice_kernel<SL>), dim3(grid), dim3(64), lds, s, A);
+  return hipGetLastError();
+}
+
 hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int items, double* env,
                           double* a_out, double* gg_out, double* cep_out, hipStream_t s) {
   if (items <= 0) return hipSuccess;
@@ -1613,6 +1818,20 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
   A.odd_zero = odd_zero; A.items = items; A.region = lpc_env_region(c.p, c.M);
   A.r = r; A.weights = c.weights; A.env_cos = c.env_cos; A.env_win = c.env_win; A.env = env;
   A.a_out = a_out; A.gg_out = gg_out; A.cep_out = cep_out;
+  const int SL = (c.p + 1 + 15) / 16;
+  if (SL <= 16 && !getenv("FDLP_LPC_LDS")) {  // lattice Durbin in registers
+    const int NAL = (c.M > c.p + 1 ? c.M : c.p + 1) + 16;
+    A.region = (NAL + c.M + 15) / 32 * 32 + 16;  // = 16 mod 32 doubles (disjoint bank halves per item)
+    const size_t lds = sizeof(double) * (4 * (size_t)A.region);
+    switch (SL) {
+#define FDLP_SL_CASE(n) case n: return launch_lpc_lattice_sl<n>(A, lds, s);
+      FDLP_SL_CASE(1) FDLP_SL_CASE(2) FDLP_SL_CASE(3) FDLP_SL_CASE(4) FDLP_SL_CASE(5) FDLP_SL_CASE(6)
+      FDLP_SL_CASE(7) FDLP_SL_CASE(8) FDLP_SL_CASE(9) FDLP_SL_CASE(10) FDLP_SL_CASE(11) FDLP_SL_CASE(12)
+      FDLP_SL_CASE(13) FDLP_SL_CASE(14) FDLP_SL_CASE(15) FDLP_SL_CASE(16)
+#undef FDLP_SL_CASE
+      default: break;
+    }
+  }
   const size_t lds = sizeof(double) * (4 * (size_t)A.region);
   switch ((c.env_nfft / 4 + 1 + 15) / 16) {  // envelope slots: u = 0 .. env_nfft/4
 #define FDLP_TS_CASE(n) case n: return launch_lpc_env_t<n>(A, lds, s);
