@@ -174,6 +174,14 @@ int fdlp_lpc_rows(fdlp_plan* plan, const double* band_dev, int32_t n_items, doub
 int fdlp_cepstrum_rows(fdlp_plan* plan, const double* a_dev, const double* gg_dev,
                        int32_t n_items, int32_t p, int32_t lim, double* cep_dev, void* stream);
 
+/* ---- global CMVN statistics (the step after feature extraction) ------------------------- */
+/* Kaldi `compute-cmvn-stats scp:feats.scp cmvn.ark` (e2e/wsj/run_fdlp_e1.sh:280; reverb :224,
+ * chime4 :193): AccCmvnStats (Kaldi transform/cmvn.cc) over `rows` feature rows [rows, dim] float32
+ * on the device, ADDED into stats_dev [2, dim+1] fp64 (row 0: sum x_d, then the frame count;
+ * row 1: sum of the float32 products x_d*x_d, then 0).  Deterministic (fixed-order reduction). */
+int fdlp_cmvn_accumulate(const float* feats_dev, int64_t rows, int32_t dim, double* stats_dev,
+                         void* stream);
+
 /* ---- host-side RNG replicas (no device work) --------------------------------------------- */
 /* CPython `random` (MT19937, init_by_array seeding, randrange(2) = getrandbits(2) with
  * rejection) -- the jitter source of computeFDLPSpectrogram.py:21,225. */
@@ -202,6 +210,20 @@ int fdlp_ark_open(const char* ark_path, const char* scp_path, fdlp_ark_writer** 
 int fdlp_ark_write(fdlp_ark_writer* w, const char* utt, const float* mat, int32_t rows,
                    int32_t cols);
 int fdlp_ark_close(fdlp_ark_writer* w);
+/* Kaldi matrix reader for `compute-cmvn-stats`-style rspecifiers: "scp:<feats.scp>" (lines
+ * "<utt> <ark path>:<offset>") or "ark:<file>" (binary ark, "-" = stdin).  Float ("FM") and double
+ * ("DM") binary matrices; data is returned as float32 (double matrices are narrowed, as Kaldi's
+ * Matrix<BaseFloat> reader does).  fdlp_mat_reader_next returns 1 with a matrix, 0 at the end,
+ * <0 on error; *key and *data stay valid until the next call. */
+typedef struct fdlp_mat_reader fdlp_mat_reader;
+int fdlp_mat_reader_open(const char* rspecifier, fdlp_mat_reader** out);
+int fdlp_mat_reader_next(fdlp_mat_reader* r, const char** key, int32_t* rows, int32_t* cols,
+                         const float** data);
+int fdlp_mat_reader_close(fdlp_mat_reader* r);
+/* Write a double matrix as a Kaldi object file (WriteKaldiObject): binary = "\0B" + "DM " + sizes
+ * + row-major fp64, or Kaldi text " [\n  v v ... \n  v v ... ]\n" (%g, the ostream default). */
+int fdlp_kaldi_write_dmatrix(const char* path, const double* m, int32_t rows, int32_t cols,
+                             int32_t binary);
 
 #ifdef __cplusplus
 }

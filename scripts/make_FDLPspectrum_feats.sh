@@ -31,6 +31,7 @@ write_utt2num_frames=false
 lifter_config=
 check_for_segment="data/train"
 ngpu=1
+compute_cmvn=false   # also write <data_dir>/cmvn.ark (global CMVN stats, fused on the device)
 seed=
 noise_seed=
 
@@ -81,9 +82,11 @@ split_list() {  # split_list <in> <out1> ... : contiguous, balanced, like utils/
 
 run_jobs() {  # run_jobs <list-pattern containing JOB> <scp-type-opt>
   local pattern=$1 stype=$2
+  local cmvn_opt=
+  $compute_cmvn && cmvn_opt="--cmvn_stats $feat_dir/cmvn_${name}.JOB.mat"
   if [ -n "$cmd" ]; then
     $cmd JOB=1:$nj "$log_dir/feats_${name}.JOB.log" \
-      python3 "$cli" "$pattern" "$feat_dir/melspec_${name}.JOB" $add_opts $stype \
+      python3 "$cli" "$pattern" "$feat_dir/melspec_${name}.JOB" $add_opts $cmvn_opt $stype \
         --fbank_type=$fbank_type --gamma_weight=$gamma_weight --add_reverb=$add_reverb \
         --add_noise=$add_noise --coeff_num=$coeff_num --coeff_range=$coeff_range --order=$order \
         --overlap_fraction=$overlap_fraction --nfilters=$nfilters --fduration=$fduration \
@@ -93,7 +96,7 @@ run_jobs() {  # run_jobs <list-pattern containing JOB> <scp-type-opt>
   local pids=() n fail=0
   for n in $(seq $nj); do
     local g=$(( (n - 1) % ngpu ))
-    HIP_VISIBLE_DEVICES=$g python3 "$cli" "${pattern//JOB/$n}" "$feat_dir/melspec_${name}.$n" $add_opts $stype \
+    HIP_VISIBLE_DEVICES=$g python3 "$cli" "${pattern//JOB/$n}" "$feat_dir/melspec_${name}.$n" $add_opts ${cmvn_opt//JOB/$n} $stype \
       --fbank_type=$fbank_type --gamma_weight=$gamma_weight --add_reverb=$add_reverb \
       --add_noise=$add_noise --coeff_num=$coeff_num --coeff_range=$coeff_range --order=$order \
       --overlap_fraction=$overlap_fraction --nfilters=$nfilters --fduration=$fduration \
@@ -137,5 +140,12 @@ fi
 
 if $write_utt2num_frames; then
   for n in $(seq $nj); do cat "$feat_dir/melspec_$name.$n.len" || exit 1; done > "$data_dir/utt2num_frames"
+fi
+if $compute_cmvn; then  # JOB partial stats -> one global cmvn.ark (a host sum; no collective needed)
+  stats_files=""
+  for n in $(seq $nj); do stats_files="$stats_files $feat_dir/cmvn_${name}.$n.mat"; done
+  PYTHONPATH="$here${PYTHONPATH:+:$PYTHONPATH}" python3 -c \
+    "import sys; from speech_recognition_tools_amd.cmvn import sum_stats_files; sum_stats_files(sys.argv[2:], sys.argv[1])" \
+    "$data_dir/cmvn.ark" $stats_files || exit 1
 fi
 echo "$0: Finished computing FDLP spectrum features for $name"

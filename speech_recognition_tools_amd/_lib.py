@@ -95,6 +95,12 @@ SIGNATURES = {
     "fdlp_ark_open": (c_i32, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(c_p)]),
     "fdlp_ark_write": (c_i32, [c_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), c_i32, c_i32]),
     "fdlp_ark_close": (c_i32, [c_p]),
+    "fdlp_cmvn_accumulate": (c_i32, [c_p, c_i64, c_i32, c_p, c_p]),
+    "fdlp_mat_reader_open": (c_i32, [ctypes.c_char_p, ctypes.POINTER(c_p)]),
+    "fdlp_mat_reader_next": (c_i32, [c_p, ctypes.POINTER(ctypes.c_char_p), P_i32, P_i32,
+                                     ctypes.POINTER(ctypes.POINTER(ctypes.c_float))]),
+    "fdlp_mat_reader_close": (c_i32, [c_p]),
+    "fdlp_kaldi_write_dmatrix": (c_i32, [ctypes.c_char_p, P_dbl, c_i32, c_i32, c_i32]),
 }
 
 

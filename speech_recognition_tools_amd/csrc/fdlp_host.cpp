@@ -15,6 +15,7 @@
 #include <climits>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/fdlp.h"
 #include "fdlp_error.h"
@@ -255,6 +256,166 @@ int fdlp_ark_close(fdlp_ark_writer* w) {
   if (w->scp && fclose(w->scp) != 0) rc = fdlp::fail(FDLP_E_IO, "scp close failed");
   delete w;
   return rc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Kaldi matrix reader ("scp:" / "ark:" rspecifiers) and double-matrix object writer, for the
+// compute-cmvn-stats drop-in (bin/compute-cmvn-stats).  Binary Kaldi format only (what copy-feats
+// and this library's ark writer produce).
+// ---------------------------------------------------------------------------------------------
+struct fdlp_mat_reader {
+  bool scp = false;
+  FILE* list = nullptr;       // scp file, or the ark stream itself for "ark:"
+  bool own_list = true;
+  FILE* cur = nullptr;        // scp: the ark file currently open
+  std::string cur_path;
+  std::string key;
+  std::vector<float> data;
+  std::vector<double> dbuf;
+};
+
+static int read_matrix_body(FILE* f, const std::string& where, std::vector<float>& out, std::vector<double>& dbuf,
+                            int32_t* rows, int32_t* cols) {
+  char hdr[2];
+  if (fread(hdr, 1, 2, f) != 2 || hdr[0] != '\0' || hdr[1] != 'B')
+    return fdlp::fail(FDLP_E_IO, "expected a binary Kaldi object at " + where);
+  char tok[4] = {0, 0, 0, 0};
+  if (fread(tok, 1, 3, f) != 3) return fdlp::fail(FDLP_E_IO, "truncated matrix header at " + where);
+  const bool is_f = !memcmp(tok, "FM ", 3), is_d = !memcmp(tok, "DM ", 3);
+  if (!is_f && !is_d) {
+    if (tok[0] == 'C' && tok[1] == 'M') return fdlp::fail(FDLP_E_IO, "compressed matrices are not supported (" + where + ")");
+    return fdlp::fail(FDLP_E_IO, "not a float/double matrix at " + where);
+  }
+  char sz;
+  int32_t r = 0, c = 0;
+  if (fread(&sz, 1, 1, f) != 1 || sz != 4 || fread(&r, 4, 1, f) != 1 || fread(&sz, 1, 1, f) != 1 || sz != 4 ||
+      fread(&c, 4, 1, f) != 1 || r < 0 || c < 0)
+    return fdlp::fail(FDLP_E_IO, "bad matrix dimensions at " + where);
+  const size_t n = (size_t)r * (size_t)c;
+  out.resize(n);
+  if (is_f) {
+    if (n && fread(out.data(), sizeof(float), n, f) != n) return fdlp::fail(FDLP_E_IO, "truncated matrix at " + where);
+  } else {
+    dbuf.resize(n);
+    if (n && fread(dbuf.data(), sizeof(double), n, f) != n) return fdlp::fail(FDLP_E_IO, "truncated matrix at " + where);
+    for (size_t i = 0; i < n; ++i) out[i] = (float)dbuf[i];
+  }
+  *rows = r;
+  *cols = c;
+  return FDLP_OK;
+}
+
+int fdlp_mat_reader_open(const char* spec, fdlp_mat_reader** out) {
+  if (!spec || !out) return fdlp::fail(FDLP_E_INVALID, "fdlp_mat_reader_open: bad args");
+  std::string s(spec);
+  // strip Kaldi rspecifier options ("scp,p:" etc.): keep the type before the first ',' or ':'
+  const size_t colon = s.find(':');
+  if (colon == std::string::npos) return fdlp::fail(FDLP_E_INVALID, "rspecifier must start with scp: or ark: (" + s + ")");
+  std::string type = s.substr(0, colon), path = s.substr(colon + 1);
+  type = type.substr(0, type.find(','));
+  if (type != "scp" && type != "ark") return fdlp::fail(FDLP_E_INVALID, "unsupported rspecifier type " + type);
+  auto* r = new (std::nothrow) fdlp_mat_reader;
+  if (!r) return fdlp::fail(FDLP_E_NOMEM, "fdlp_mat_reader_open: out of memory");
+  r->scp = type == "scp";
+  if (path == "-") {
+    r->list = stdin;
+    r->own_list = false;
+  } else {
+    r->list = fopen(path.c_str(), r->scp ? "r" : "rb");
+  }
+  if (!r->list) {
+    delete r;
+    return fdlp::fail(FDLP_E_IO, "cannot open " + path);
+  }
+  *out = r;
+  return FDLP_OK;
+}
+
+int fdlp_mat_reader_next(fdlp_mat_reader* r, const char** key, int32_t* rows, int32_t* cols, const float** data) {
+  if (!r || !key || !rows || !cols || !data) return fdlp::fail(FDLP_E_INVALID, "fdlp_mat_reader_next: bad args");
+  if (r->scp) {
+    char line[65536];
+    for (;;) {
+      if (!fgets(line, sizeof line, r->list)) return 0;
+      std::string l(line);
+      while (!l.empty() && (l.back() == '\n' || l.back() == '\r' || l.back() == ' ' || l.back() == '\t')) l.pop_back();
+      size_t a = l.find_first_not_of(" \t");
+      if (a == std::string::npos) continue;  // blank line
+      size_t b = l.find_first_of(" \t", a);
+      if (b == std::string::npos) return fdlp::fail(FDLP_E_IO, "bad scp line: " + l);
+      r->key = l.substr(a, b - a);
+      std::string rx = l.substr(l.find_first_not_of(" \t", b));
+      std::string file = rx;
+      long off = -1;
+      const size_t c = rx.rfind(':');
+      if (c != std::string::npos && c + 1 < rx.size() && rx.find_first_not_of("0123456789", c + 1) == std::string::npos) {
+        file = rx.substr(0, c);
+        off = atol(rx.c_str() + c + 1);
+      }
+      if (!r->cur || file != r->cur_path) {
+        if (r->cur) fclose(r->cur);
+        r->cur = fopen(file.c_str(), "rb");
+        r->cur_path = file;
+        if (!r->cur) return fdlp::fail(FDLP_E_IO, "cannot open " + file);
+      }
+      if (fseek(r->cur, off < 0 ? 0 : off, SEEK_SET) != 0) return fdlp::fail(FDLP_E_IO, "cannot seek in " + file);
+      int rc = read_matrix_body(r->cur, rx, r->data, r->dbuf, rows, cols);
+      if (rc != FDLP_OK) return rc;
+      break;
+    }
+  } else {
+    // "<key> " then the binary object
+    std::string k;
+    int ch;
+    while ((ch = fgetc(r->list)) != EOF && (ch == ' ' || ch == '\n' || ch == '\t' || ch == '\r')) {}
+    if (ch == EOF) return 0;
+    do { k.push_back((char)ch); } while ((ch = fgetc(r->list)) != EOF && ch != ' ');
+    if (ch == EOF) return fdlp::fail(FDLP_E_IO, "truncated ark after key " + k);
+    r->key = k;
+    int rc = read_matrix_body(r->list, "ark key " + k, r->data, r->dbuf, rows, cols);
+    if (rc != FDLP_OK) return rc;
+  }
+  *key = r->key.c_str();
+  *data = r->data.data();
+  return 1;
+}
+
+int fdlp_mat_reader_close(fdlp_mat_reader* r) {
+  if (!r) return FDLP_OK;
+  if (r->cur) fclose(r->cur);
+  if (r->list && r->own_list) fclose(r->list);
+  delete r;
+  return FDLP_OK;
+}
+
+int fdlp_kaldi_write_dmatrix(const char* path, const double* m, int32_t rows, int32_t cols, int32_t binary) {
+  if (!path || rows < 0 || cols < 0 || (rows * (int64_t)cols > 0 && !m))
+    return fdlp::fail(FDLP_E_INVALID, "fdlp_kaldi_write_dmatrix: bad args");
+  FILE* f = fopen(path, binary ? "wb" : "w");
+  if (!f) return fdlp::fail(FDLP_E_IO, std::string("cannot open ") + path);
+  int ok = 1;
+  if (binary) {
+    const char hdr[] = {'\0', 'B', 'D', 'M', ' '};
+    const char four = 4;
+    ok &= fwrite(hdr, 1, 5, f) == 5;
+    ok &= fwrite(&four, 1, 1, f) == 1;
+    ok &= fwrite(&rows, 4, 1, f) == 1;
+    ok &= fwrite(&four, 1, 1, f) == 1;
+    ok &= fwrite(&cols, 4, 1, f) == 1;
+    const size_t n = (size_t)rows * (size_t)cols;
+    if (n) ok &= fwrite(m, sizeof(double), n, f) == n;
+  } else if (cols == 0 || rows == 0) {
+    ok &= fputs(" [ ]\n", f) >= 0;
+  } else {  // Kaldi MatrixBase::Write text mode
+    ok &= fputs(" [", f) >= 0;
+    for (int32_t i = 0; i < rows; ++i) {
+      ok &= fputs("\n  ", f) >= 0;
+      for (int32_t j = 0; j < cols; ++j) ok &= fprintf(f, "%g ", m[(size_t)i * cols + j]) >= 0;
+    }
+    ok &= fputs("]\n", f) >= 0;
+  }
+  if (fclose(f) != 0) ok = 0;
+  return ok ? FDLP_OK : fdlp::fail(FDLP_E_IO, std::string("write failed: ") + path);
 }
 
 }  // extern "C"

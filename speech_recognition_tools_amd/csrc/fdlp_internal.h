@@ -104,4 +104,6 @@ constexpr int kDftMaxSub = 512;  // longest LDS-resident sub-DFT of the four-ste
 hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc* frames,
                           const UttDesc* utts, int n_utt, int maxL, float* out,
                           double* out_f64, int decimals, hipStream_t s);
+int cmvn_chunks(int64_t rows);
+hipError_t launch_cmvn(const float* x, int64_t rows, int D, double* part, double* stats, hipStream_t s);
 }  // namespace fdlp

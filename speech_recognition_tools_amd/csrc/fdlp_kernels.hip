@@ -1855,4 +1855,59 @@ hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc
   return hipGetLastError();
 }
 
+// -----------------------------------------------------------------------------------------
+// 8. Global CMVN statistics: Kaldi compute-cmvn-stats (no --spk2utt) -> AccCmvnStats
+//    (transform/cmvn.cc), the step after feature extraction in e2e/wsj/run_fdlp_e1.sh:280:
+//      stats[0][d] += x_d,  stats[1][d] += x_d * x_d  (a BaseFloat product: float32, then double),
+//      stats[0][D] += 1 per frame.
+//    Deterministic: chunk partial sums in row order, then a fixed-order sum over chunks, so the
+//    result does not depend on scheduling.  HBM-bound (4 bytes per feature read once).
+// -----------------------------------------------------------------------------------------
+constexpr int kCmvnRows = 256;  // rows per chunk
+
+__global__ __launch_bounds__(128) void cmvn_partial_kernel(const float* __restrict__ x, int64_t rows, int D,
+                                                           double* __restrict__ part) {
+  const int64_t r0 = (int64_t)blockIdx.x * kCmvnRows;
+  const int64_t r1 = min(rows, r0 + (int64_t)kCmvnRows);
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    double s0 = 0.0, q0 = 0.0;
+    const float* col = x + r0 * D + d;
+    for (int64_t r = r0; r < r1; ++r, col += D) {
+      const float v = *col;
+      const float v2 = v * v;  // BaseFloat product, as Kaldi forms it
+      s0 += (double)v;
+      q0 += (double)v2;
+    }
+    part[((int64_t)blockIdx.x * 2) * D + d] = s0;
+    part[((int64_t)blockIdx.x * 2 + 1) * D + d] = q0;
+  }
+}
+
+__global__ __launch_bounds__(128) void cmvn_finish_kernel(const double* __restrict__ part, int nchunks, int D,
+                                                          int64_t rows, double* __restrict__ stats) {
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    double s = 0.0, q = 0.0;
+    for (int c = 0; c < nchunks; ++c) {
+      s += part[((int64_t)c * 2) * D + d];
+      q += part[((int64_t)c * 2 + 1) * D + d];
+    }
+    stats[d] += s;
+    stats[(D + 1) + d] += q;
+  }
+  if (threadIdx.x == 0) stats[D] += (double)rows;
+}
+
+int cmvn_chunks(int64_t rows) { return (int)((rows + kCmvnRows - 1) / kCmvnRows); }
+
+hipError_t launch_cmvn(const float* x, int64_t rows, int D, double* part, double* stats, hipStream_t s) {
+  const int nch = cmvn_chunks(rows);
+  if (nch > 0) {
+    hipLaunchKernelGGL(cmvn_partial_kernel, dim3(nch), dim3(128), 0, s, x, rows, D, part);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(cmvn_finish_kernel, dim3(1), dim3(128), 0, s, part, nch, D, rows, stats);
+  return hipGetLastError();
+}
+
 }  // namespace fdlp

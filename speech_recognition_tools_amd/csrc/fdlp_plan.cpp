@@ -858,4 +858,18 @@ int fdlp_cepstrum_rows(fdlp_plan* p, const double* a, const double* gg, int32_t 
   return FDLP_OK;
 }
 
+int fdlp_cmvn_accumulate(const float* feats, int64_t rows, int32_t dim, double* stats, void* stream) {
+  if (rows < 0 || dim <= 0 || !stats || (rows > 0 && !feats)) return fail(FDLP_E_INVALID, "fdlp_cmvn_accumulate: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t nch = (size_t)fdlp::cmvn_chunks(rows);
+  double* part = nullptr;
+  // stream-ordered scratch for the per-chunk partial sums [nch, 2, dim]
+  HIP_TRY(hipMallocAsync((void**)&part, sizeof(double) * 2 * (size_t)dim * std::max<size_t>(nch, 1), s));
+  hipError_t e = fdlp::launch_cmvn(feats, rows, dim, part, stats, s);
+  hipError_t e2 = hipFreeAsync(part, s);
+  if (e != hipSuccess) return fail(FDLP_E_HIP, std::string("cmvn kernels: ") + hipGetErrorString(e));
+  if (e2 != hipSuccess) return fail(FDLP_E_HIP, std::string("hipFreeAsync: ") + hipGetErrorString(e2));
+  return FDLP_OK;
+}
+
 }  // extern "C"

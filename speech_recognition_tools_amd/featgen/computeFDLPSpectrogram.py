@@ -60,6 +60,9 @@ def build_parser():
                         help="decimals of the reference's text ark ('%%.3f'); -1 keeps full float32")
     parser.add_argument('--support_eps', type=float, default=None,
                         help='filter taps below eps*peak are skipped in the autocorrelation (0 = exact)')
+    parser.add_argument('--cmvn_stats', type=str, default=None,
+                        help='also write the global CMVN stats of the written features (Kaldi compute-cmvn-stats '
+                             'format, accumulated on the device) to this file')
     return parser
 
 
@@ -135,6 +138,10 @@ def getFeats(args, srate=16000, window=np.hamming):
     noise_rng = NpRandom(args.noise_seed) if noise is not None else None
     noise_dev = torch.from_numpy(np.ascontiguousarray(noise)).cuda(device) if noise is not None else None
 
+    cmvn = None
+    if args.cmvn_stats:  # fused e2e/*/run_fdlp_e1.sh `compute-cmvn-stats` (speech_recognition_tools_amd.cmvn)
+        from speech_recognition_tools_amd.cmvn import CmvnAccumulator
+        cmvn = CmvnAccumulator(cfg.nfilters, device)
     all_feats = OrderedDict()
     all_lens = OrderedDict()
     pending = []  # (uttid, samples, F, noise_off, alpha)
@@ -152,6 +159,8 @@ def getFeats(args, srate=16000, window=np.hamming):
             kw = dict(noise=noise_dev, noise_off=[x[3] for x in pending], noise_alpha=[x[4] for x in pending])
         out, rows, _ = plan.compute(torch.from_numpy(pcm).cuda(device), lens, jit, ark_decimals=args.ark_precision,
                                     preprocess="diff" if diff else None, **kw)
+        if cmvn is not None:
+            cmvn.add(out[:int(rows[-1])])
         host = out.cpu().numpy()
         for i, x in enumerate(pending):
             all_feats[x[0]] = host[rows[i]:rows[i + 1]]                   # :227
@@ -193,6 +202,9 @@ def getFeats(args, srate=16000, window=np.hamming):
             pending_frames += F
     flush()
     dict2Ark(all_feats, outfile, args.kaldi_cmd)                            # :231
+    if cmvn is not None:
+        from speech_recognition_tools_amd.cmvn import write_kaldi_dmatrix
+        write_kaldi_dmatrix(args.cmvn_stats, cmvn.numpy(), binary=True)
     if args.write_utt2num_frames:                                           # :232-237
         with open(outfile + '.len', 'w+') as file:
             for key, lens in all_lens.items():

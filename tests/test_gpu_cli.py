@@ -126,7 +126,7 @@ def test_driver_script_two_jobs(tmp_path):
            "--nfilters", str(o["nfilters"]), "--order", str(o["order"]), "--fduration", str(o["fduration"]),
            "--frate", str(o["frate"]), "--coeff_range", o["coeff_range"], "--coeff_num", str(o["coeff_num"]),
            "--overlap_fraction", str(o["overlap_fraction"]), "--fbank_type", o["fbank_type"],
-           "--write_utt2num_frames", "true", str(data), str(tmp_path / "fbank")]
+           "--write_utt2num_frames", "true", "--compute_cmvn", "true", str(data), str(tmp_path / "fbank")]
     r = subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     feats = [l.split() for l in open(str(data / "feats.scp"))]
@@ -139,3 +139,10 @@ def test_driver_script_two_jobs(tmp_path):
         arks.update(read_ark(str(tmp_path / "fbank" / ("melspec_test_set.%d.ark" % n))))
     for u in meta["utts"]:
         assert arks[u].shape == ref[u].shape
+    # fused global CMVN: the JOB stats summed into data_dir/cmvn.ark == Kaldi semantics over the arks
+    from oracle import cmvn_oracle as CO
+    from speech_recognition_tools_amd.cmvn import read_kaldi_dmatrix
+    got = read_kaldi_dmatrix(str(data / "cmvn.ark"))
+    want = CO.global_stats(arks[u] for u in meta["utts"])
+    assert got[0, -1] == want[0, -1]
+    assert np.max(np.abs(got - want) / np.maximum(np.abs(want), 1.0)) <= 1e-12
