@@ -1341,7 +1341,18 @@ __global__ __launch_bounds__(64, 4) void lpc_env_lattice_kernel(LpcEnvArgs A_) {
   extern __shared__ double sh[];
   const LpcEnvArgs& A = A_;
   const int ngroups = (A.items + 3) >> 2;
+  // (prefetching the next group's r into registers before the envelope phase was measured: no gain,
+  // it costs a wave per SIMD of occupancy)
+  double Rn[SL], r0n;
+  auto load_r = [&](int grp) {
+    const int it = grp * 4 + (threadIdx.x >> 4);
+    const double* rr = A.r + (int64_t)(it < A.items ? it : 0) * A.nlags;
+#pragma unroll
+    for (int s = 0; s < SL; ++s) Rn[s] = rr[min((int)(threadIdx.x & 15) + 16 * s + 1, A.nlags - 1)];
+    r0n = rr[0];
+  };
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    load_r(grp);
     // Everything below is re-derived per group from opaque copies, so the compiler cannot hoist
     // group-invariant addresses/tables out of the loop (they would stay live through the Durbin phase).
     int tid = threadIdx.x, p = A.p, M = A.M;
@@ -1350,7 +1361,6 @@ __global__ __launch_bounds__(64, 4) void lpc_env_lattice_kernel(LpcEnvArgs A_) {
     const int g = tid >> 4;
     const int l = tid & 15;
     const bool lane0 = l == 0;
-    const int nlags = A.nlags;
     const int NAL = (M > p + 1 ? M : p + 1) + 16;
     double* la = sh + g * A.region;  // a_0..a_p, zeros up to NAL
     double* cs = la + NAL;           // c_0..c_{M-1}
@@ -1360,17 +1370,14 @@ __global__ __launch_bounds__(64, 4) void lpc_env_lattice_kernel(LpcEnvArgs A_) {
     const bool valid = item < A.items;
     // ---- phase 1: Levinson-Durbin (features.py:226-228) in registers -------------------------
     double Av[SL], Bv[SL], R1[SL];
-    const double* rr = A.r + (int64_t)(valid ? item : 0) * nlags;
 #pragma unroll
-    for (int s = 0; s < SL; ++s) {  // branch-free: clamped loads, then select
+    for (int s = 0; s < SL; ++s) {  // branch-free: clamped loads (load_r), then select
       const int m = l + 16 * s;
-      const double v = rr[min(m + 1, nlags - 1)];
-      R1[s] = (valid && m <= p) ? v : 0.0;
+      R1[s] = (valid && m <= p) ? Rn[s] : 0.0;
       Av[s] = (m == 0) ? 1.0 : 0.0;
       Bv[s] = Av[s];
     }
-    const double r0v = rr[0];
-    const double r0 = valid ? r0v : 1.0;
+    const double r0 = valid ? r0n : 1.0;
     double E = r0;
     if (FDLP_LPC_PHASES & 1) lattice_durbin<SL, 0>(Av, Bv, R1, E, p, lane0);
     double part = 0.0;
@@ -1391,10 +1398,19 @@ __global__ __launch_bounds__(64, 4) void lpc_env_lattice_kernel(LpcEnvArgs A_) {
     for (int b0 = 0; b0 < ((FDLP_LPC_PHASES & 2) ? M : 0); b0 += 16) {
       const int n = b0 + l;
       const double inv_n = 1.0 / (double)(n > 0 ? n : 1);
-      double acc = 0.0;
+      // finished blocks: four independent FMA chains (the trip count is uniform across the wave)
       const int kstart = max(1, b0 - p);
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      int k = kstart;
       double kd = (double)kstart;
-      for (int k = kstart; k < b0; ++k, kd += 1.0) acc = fma(kd * cs[k], la[n - k], acc);
+      for (; k + 3 < b0; k += 4, kd += 4.0) {
+        a0 = fma(kd * cs[k], la[n - k], a0);
+        a1 = fma((kd + 1.0) * cs[k + 1], la[n - k - 1], a1);
+        a2 = fma((kd + 2.0) * cs[k + 2], la[n - k - 2], a2);
+        a3 = fma((kd + 3.0) * cs[k + 3], la[n - k - 3], a3);
+      }
+      for (; k < b0; ++k, kd += 1.0) a0 = fma(kd * cs[k], la[n - k], a0);
+      double acc = (a0 + a1) + (a2 + a3);
       double mine = 0.0;
       cep_block_step<0>(b0, M, l, gg, inv_n, la, n, acc, mine);
       if (n < M) {

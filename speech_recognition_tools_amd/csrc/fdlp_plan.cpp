@@ -687,7 +687,7 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
   HIP_TRY(hipEventRecord(p->staging_done, s));
   p->staging_pending = true;
 
-  const int items = (int)nf * p->B;
+
   // Sub-batches alternate between the caller's stream and the plan's second stream so that the
   // MFMA-bound autocorrelation of one overlaps the VALU-bound DFT / LPC kernels of the other.
   const int nsub = (int)std::max<int64_t>(1, std::min<int64_t>(p->pipeline, nf / 256));
