@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""End-to-end throughput of compute-fdlp-feats (WAV files in, Kaldi ark/scp out) on one MI355X, i.e.
+including the host side the device-resident bench.py excludes: WAV read + parse, jitter RNG, H2D,
+D2H and the ark writer.  Synthetic speech-like 4 s WAVs (bench.speech_like_batch) in a temp dir.
+
+    python benchmarks/cli_throughput.py [--utts 512] [--workers 1 4 8] [--batch-frames 8192]
+Prints one JSON line per worker count.
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+from scipy.io import wavfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--utts", type=int, default=512)
+    ap.add_argument("--seconds", type=float, default=4.0)
+    ap.add_argument("--workers", type=int, nargs="+", default=[1, 4, 8])
+    ap.add_argument("--batch-frames", type=int, default=8192)
+    a = ap.parse_args()
+    from bench import speech_like_batch
+    from speech_recognition_tools_amd.featgen.computeFDLPSpectrogram import build_parser, getFeats
+    T = int(a.seconds * 16000)
+    with tempfile.TemporaryDirectory() as d:
+        sig = speech_like_batch(a.utts, T, 77)
+        with open(os.path.join(d, "wav.scp"), "w") as f:
+            for i in range(a.utts):
+                p = os.path.join(d, "u%05d.wav" % i)
+                wavfile.write(p, 16000, sig[i])
+                f.write("u%05d %s\n" % (i, p))
+        opts = ["--nfilters=80", "--coeff_num=100", "--coeff_range=0,100", "--order=150", "--fduration=1.5",
+                "--frate=100", "--overlap_fraction=0.25", "--fbank_type=cochlear,1,1,1,2.5,1", "--seed=1",
+                "--batch_frames=%d" % a.batch_frames]
+        devnull = open(os.devnull, "w")
+        # warm-up (plan build, kernel load)
+        so = sys.stdout
+        sys.stdout = devnull
+        getFeats(build_parser().parse_args([os.path.join(d, "wav.scp"), os.path.join(d, "warm")] + opts),
+                 return_feats=False)
+        sys.stdout = so
+        for w in a.workers:
+            args = build_parser().parse_args([os.path.join(d, "wav.scp"), os.path.join(d, "o%d" % w),
+                                              "--io_workers=%d" % w] + opts)
+            sys.stdout = devnull
+            t0 = time.perf_counter()
+            getFeats(args, return_feats=False)
+            el = time.perf_counter() - t0
+            sys.stdout = so
+            audio_h = a.utts * T / 16000.0 / 3600.0
+            print(json.dumps({"metric": "compute-fdlp-feats end-to-end audio-hours/s (WAV in, ark out)",
+                              "value": audio_h / el, "unit": "audio-hours/s", "io_workers": w,
+                              "utts": a.utts, "utt_seconds": a.seconds, "seconds": el,
+                              "ark_bytes": os.path.getsize(os.path.join(d, "o%d.ark" % w))}))
+            sys.stdout.flush()
+
+
+if __name__ == "__main__":
+    main()

@@ -118,7 +118,9 @@ if [ -f "$segment" ]; then
   else
     scp_dump_name=$log_dir/segment_dump/${name}_segmentdump
     mkdir -p "$log_dir/segment_dump"
-    extract-segments scp,p:$scp $segment ark,scp:${scp_dump_name}.ark,${scp_dump_name}.scp || exit 1
+    xseg=extract-segments
+    command -v extract-segments >/dev/null 2>&1 || xseg="$here/bin/extract-segments"  # no Kaldi on PATH
+    $xseg scp,p:$scp $segment ark,scp:${scp_dump_name}.ark,${scp_dump_name}.scp || exit 1
   fi
   split_segments=""
   for n in $(seq $nj); do split_segments="$split_segments $log_dir/segments.$n"; done

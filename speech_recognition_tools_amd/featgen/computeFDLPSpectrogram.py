@@ -12,8 +12,8 @@ skip/abort semantics as the reference.  Differences (DESIGN.md "CLI"):
   * a failure to write the ark exits non-zero (the reference ignores copy-feats' status).
 """
 import argparse
+import collections
 import os
-import subprocess
 import sys
 import time
 from collections import OrderedDict
@@ -24,8 +24,7 @@ if __package__ in (None, ""):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from speech_recognition_tools_amd.featgen import features  # noqa: E402
-from speech_recognition_tools_amd.featgen.features import (add_noise_to_wav_params, dict2Ark,  # noqa: E402
-                                                           load_noise, read_wav_bytes)
+from speech_recognition_tools_amd.featgen.features import add_noise_to_wav_params, load_noise  # noqa: E402
 
 
 def build_parser():
@@ -60,6 +59,8 @@ def build_parser():
                         help="decimals of the reference's text ark ('%%.3f'); -1 keeps full float32")
     parser.add_argument('--support_eps', type=float, default=None,
                         help='filter taps below eps*peak are skipped in the autocorrelation (0 = exact)')
+    parser.add_argument('--io_workers', type=int, default=4,
+                        help='threads reading/parsing the scp entries ahead of the device (1 = inline)')
     parser.add_argument('--cmvn_stats', type=str, default=None,
                         help='also write the global CMVN stats of the written features (Kaldi compute-cmvn-stats '
                              'format, accumulated on the device) to this file')
@@ -68,33 +69,13 @@ def build_parser():
 
 def _read_scp_entry(line, scp_type):
     """(uttid, int16 samples, sr) or (uttid, None, None) on a read failure (skip, :129-154)."""
-    tokens = line.strip().split()
-    uttid, inwav = tokens[0], ' '.join(tokens[1:])
-    try:
-        if scp_type == 'wav':
-            if inwav[-1] == '|':                                            # :130-134
-                proc = subprocess.run(inwav[:-1], shell=True, stdout=subprocess.PIPE)
-                data = proc.stdout
-            else:                                                           # :138-139
-                with open(inwav, 'rb') as f:
-                    data = f.read()
-        elif scp_type == 'segment':                                         # :145-149
-            proc = subprocess.run('wav-copy ' + inwav + ' - ', shell=True, stdout=subprocess.PIPE)
-            data = proc.stdout
-        else:
-            raise ValueError('Invalid type of scp type, it should be either wav or segment')
-        sr, sig = read_wav_bytes(data)
-        return uttid, sig, sr
-    except ValueError as e:
-        if 'Invalid type of scp type' in str(e):
-            raise
-        return uttid, None, None
-    except Exception:
-        return uttid, None, None
+    from speech_recognition_tools_amd.io_pipeline import read_rx
+    return read_rx(line, scp_type)
 
 
-def getFeats(args, srate=16000, window=np.hamming):
-    """computeFDLPSpectrogram.py:29-237 on the device."""
+def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
+    """computeFDLPSpectrogram.py:29-237 on the device.  Returns {utt: features} (float32, as written to
+    the ark) unless return_feats is False (the CLI: features are streamed to the ark only)."""
     if window is not np.hamming:
         raise ValueError("only the reference's np.hamming analysis window is supported")
     import torch
@@ -137,15 +118,31 @@ def getFeats(args, srate=16000, window=np.hamming):
     jit_rng = PyRandom(args.seed)
     noise_rng = NpRandom(args.noise_seed) if noise is not None else None
     noise_dev = torch.from_numpy(np.ascontiguousarray(noise)).cuda(device) if noise is not None else None
-
     cmvn = None
     if args.cmvn_stats:  # fused e2e/*/run_fdlp_e1.sh `compute-cmvn-stats` (speech_recognition_tools_amd.cmvn)
         from speech_recognition_tools_amd.cmvn import CmvnAccumulator
         cmvn = CmvnAccumulator(cfg.nfilters, device)
-    all_feats = OrderedDict()
+    from speech_recognition_tools_amd.io_pipeline import ArkStream, PrefetchReader
+
+    all_feats = OrderedDict() if return_feats else None
     all_lens = OrderedDict()
+    ark = ArkStream(outfile)                                                # :231 (streamed)
+    # Two batches in flight: while the device works on one, the host reads/parses the next
+    # (PrefetchReader threads) and writes the ark entries of the previous one.
+    inflight = collections.deque()  # (entries, rows, host_out, event)
     pending = []  # (uttid, samples, F, noise_off, alpha)
     pending_frames = 0
+
+    def complete(job):
+        entries, rows, host, ev = job
+        ev.synchronize()
+        for i, x in enumerate(entries):
+            feat = host[rows[i]:rows[i + 1]]
+            ark.write(x[0], feat)
+            if all_feats is not None:
+                all_feats[x[0]] = feat.copy()                              # :227
+            if args.write_utt2num_frames:
+                all_lens[x[0]] = int(rows[i + 1] - rows[i])               # :228-229
 
     def flush():
         nonlocal pending, pending_frames
@@ -153,27 +150,28 @@ def getFeats(args, srate=16000, window=np.hamming):
             return
         lens = [x[1].shape[0] for x in pending]
         jit = np.concatenate([jit_rng.randbits2(x[2] - 1) for x in pending])
-        pcm = np.concatenate([x[1] for x in pending])
+        pcm_host = torch.from_numpy(np.concatenate([x[1] for x in pending])).pin_memory()
+        pcm = pcm_host.to(torch.device("cuda", device), non_blocking=True)
         kw = {}
         if noise is not None:
             kw = dict(noise=noise_dev, noise_off=[x[3] for x in pending], noise_alpha=[x[4] for x in pending])
-        out, rows, _ = plan.compute(torch.from_numpy(pcm).cuda(device), lens, jit, ark_decimals=args.ark_precision,
+        out, rows, _ = plan.compute(pcm, lens, jit, ark_decimals=args.ark_precision,
                                     preprocess="diff" if diff else None, **kw)
         if cmvn is not None:
             cmvn.add(out[:int(rows[-1])])
-        host = out.cpu().numpy()
-        for i, x in enumerate(pending):
-            all_feats[x[0]] = host[rows[i]:rows[i + 1]]                   # :227
-            if args.write_utt2num_frames:
-                all_lens[x[0]] = int(rows[i + 1] - rows[i])               # :228-229
+        host = torch.empty(out.shape, dtype=out.dtype, pin_memory=True)
+        host.copy_(out, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        inflight.append((pending, rows, host.numpy(), ev))
         pending, pending_frames = [], 0
+        while len(inflight) > 1:
+            complete(inflight.popleft())
 
     sr = None
-    with open(wavs, 'r') as fid:
-        for line in fid:                                                    # :125
-            if not line.strip():
-                continue
-            uttid, sig, sr_new = _read_scp_entry(line, scp_type)
+    workers = max(1, int(getattr(args, 'io_workers', 4) or 1))
+    try:
+        for uttid, sig, sr_new in PrefetchReader(wavs, scp_type, workers=workers):   # :125
             skip = sig is None
             if not skip:
                 sr = sr_new
@@ -197,19 +195,24 @@ def getFeats(args, srate=16000, window=np.hamming):
             if pending_frames + F > plan.max_frames:
                 flush()
             if F > plan.max_frames:
+                while inflight:
+                    complete(inflight.popleft())
                 plan = FdlpPlan(cfg, device=device, max_frames=F)
             pending.append((uttid, sig, F, off, alpha))
             pending_frames += F
-    flush()
-    dict2Ark(all_feats, outfile, args.kaldi_cmd)                            # :231
-    if cmvn is not None:
-        from speech_recognition_tools_amd.cmvn import write_kaldi_dmatrix
-        write_kaldi_dmatrix(args.cmvn_stats, cmvn.numpy(), binary=True)
+        flush()
+        while inflight:
+            complete(inflight.popleft())
+    finally:
+        ark.close()
     if args.write_utt2num_frames:                                           # :232-237
         with open(outfile + '.len', 'w+') as file:
             for key, lens in all_lens.items():
                 file.write("{:s} {:d}".format(key, lens))
                 file.write("\n")
+    if cmvn is not None:
+        from speech_recognition_tools_amd.cmvn import write_kaldi_dmatrix
+        write_kaldi_dmatrix(args.cmvn_stats, cmvn.numpy(), binary=True)
     return all_feats
 
 
@@ -218,7 +221,7 @@ def main(argv=None):
     start_time = time.time()
     print('%s: Extracting features....' % sys.argv[0])
     sys.stdout.flush()
-    getFeats(args)
+    getFeats(args, return_feats=False)
     print('Execution Time: {t:.3f} seconds'.format(t=time.time() - start_time))
     sys.stdout.flush()
 
