@@ -174,6 +174,31 @@ int fdlp_lpc_rows(fdlp_plan* plan, const double* band_dev, int32_t n_items, doub
 int fdlp_cepstrum_rows(fdlp_plan* plan, const double* a_dev, const double* gg_dev,
                        int32_t n_items, int32_t p, int32_t lim, double* cep_dev, void* stream);
 
+/* ---- augmentation: addReverb (features.py:110-115) -------------------------------------- */
+/* --add_reverb small_room|medium_room|large_room (computeFDLPSpectrogram.py:75-91, :168-170): after the
+ * optional diff / noise preprocessing, every utterance is convolved with the RIR (channel 1 of
+ * ./RIR/<room>.wav / 2^15) and re-aligned on the argmax of np.correlate(x, y, 'valid').  Writes the
+ * fp64 signals to out_dev at the same offsets as the input (feed them to fdlp_compute as
+ * FDLP_PCM_F64 with preprocess NONE and no noise) and their lengths to out_len (T, or T-1 in the
+ * reference's edge case of a best shift of R-1).  Synchronous: waits for `stream` to return the
+ * lengths. */
+typedef struct fdlp_reverb_batch {
+  int32_t n_utt;
+  int32_t pcm_kind;              /* FDLP_PCM_I16 | FDLP_PCM_F64 (f64: no preprocessing)            */
+  const void* pcm_dev;
+  const int64_t* pcm_off;        /* host [n_utt] */
+  const int64_t* utt_len;        /* host [n_utt] */
+  int32_t preprocess;            /* FDLP_PRE_DIFF or FDLP_PRE_NONE (int16 input only)              */
+  const int16_t* noise_dev;      /* nullable: x = s + alpha * noise[off:off+T] before the reverb    */
+  const int64_t* noise_off;      /* host [n_utt] */
+  const double* noise_alpha;     /* host [n_utt] */
+  const double* rir_dev;         /* device [rir_len] */
+  int32_t rir_len;
+  double* out_dev;               /* device f64, indexed like pcm_dev                              */
+  int64_t* out_len;              /* host [n_utt] */
+} fdlp_reverb_batch;
+int fdlp_reverb(const fdlp_reverb_batch* batch, void* stream);
+
 /* ---- global CMVN statistics (the step after feature extraction) ------------------------- */
 /* Kaldi `compute-cmvn-stats scp:feats.scp cmvn.ark` (e2e/wsj/run_fdlp_e1.sh:280; reverb :224,
  * chime4 :193): AccCmvnStats (Kaldi transform/cmvn.cc) over `rows` feature rows [rows, dim] float32

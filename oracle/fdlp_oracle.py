@@ -342,6 +342,21 @@ def add_noise(sig, noise, snr, u):
     return sig + alp * noise[off:off + len(sig)]
 
 
+def add_reverb(sig: np.ndarray, rir: np.ndarray) -> np.ndarray:
+    """addReverb (features.py:110-115): full convolution with the RIR, then the T samples that start one
+    past the best-correlated shift: np.correlate(sig, out, 'valid')[k] = sum_n sig[n] out[n + R-1-k], so
+    indM = R - argmax = s* + 1 with s* the largest shift attaining the maximum."""
+    out = np.convolve(sig, rir)
+    xxc = np.correlate(sig, out, 'valid')
+    indM = len(xxc) - np.argmax(xxc)
+    return out[indM:indM + len(sig)]
+
+
+def load_rir(stereo_int16: np.ndarray) -> np.ndarray:
+    """RIR as the reference loads it (computeFDLPSpectrogram.py:75-87): channel 1 of the stereo WAV / 2**15."""
+    return stereo_int16[:, 1] / np.power(2, 15)
+
+
 # --------------------------------------------------------------------------------------
 # whole pipeline
 # --------------------------------------------------------------------------------------
@@ -408,7 +423,8 @@ class FdlpOracle:
 
 def compute_utterances(cfg: FdlpConfig, signals: Dict[str, np.ndarray], seed: int,
                        noise: Optional[np.ndarray] = None, snr: Optional[float] = None,
-                       noise_seed: Optional[int] = None, diff: bool = False) -> Dict[str, np.ndarray]:
+                       noise_seed: Optional[int] = None, diff: bool = False,
+                       rir: Optional[np.ndarray] = None) -> Dict[str, np.ndarray]:
     """getFeats over an ordered dict of int16 signals with a seeded jitter stream
     (random.seed(seed), :21,:225) and optionally seeded noise mixing (np.random.seed)."""
     orc = FdlpOracle(cfg)
@@ -421,5 +437,7 @@ def compute_utterances(cfg: FdlpConfig, signals: Dict[str, np.ndarray], seed: in
             x = diff_signal(sig)
         elif noise is not None:
             x = add_noise(sig, noise, snr, nrng.rand())
+        if rir is not None:                                            # :168-170
+            x = add_reverb(x, rir)
         out[utt] = orc.utterance(x, rng)
     return out

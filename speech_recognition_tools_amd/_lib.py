@@ -60,6 +60,14 @@ class FdlpBatchC(ctypes.Structure):
     ]
 
 
+class FdlpReverbBatchC(ctypes.Structure):
+    _fields_ = [
+        ("n_utt", c_i32), ("pcm_kind", c_i32), ("pcm_dev", c_p), ("pcm_off", P_i64), ("utt_len", P_i64),
+        ("preprocess", c_i32), ("noise_dev", c_p), ("noise_off", P_i64), ("noise_alpha", P_dbl),
+        ("rir_dev", c_p), ("rir_len", c_i32), ("out_dev", c_p), ("out_len", P_i64),
+    ]
+
+
 # name -> (restype, argtypes); every function declared in include/fdlp.h
 SIGNATURES = {
     "fdlp_plan_create": (c_i32, [ctypes.POINTER(FdlpConfigC), c_i32, ctypes.POINTER(c_p)]),
@@ -96,6 +104,7 @@ SIGNATURES = {
     "fdlp_ark_write": (c_i32, [c_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), c_i32, c_i32]),
     "fdlp_ark_close": (c_i32, [c_p]),
     "fdlp_cmvn_accumulate": (c_i32, [c_p, c_i64, c_i32, c_p, c_p]),
+    "fdlp_reverb": (c_i32, [ctypes.POINTER(FdlpReverbBatchC), c_p]),
     "fdlp_mat_reader_open": (c_i32, [ctypes.c_char_p, ctypes.POINTER(c_p)]),
     "fdlp_mat_reader_next": (c_i32, [c_p, ctypes.POINTER(ctypes.c_char_p), P_i32, P_i32,
                                      ctypes.POINTER(ctypes.POINTER(ctypes.c_float))]),

@@ -104,6 +104,14 @@ constexpr int kDftMaxSub = 512;  // longest LDS-resident sub-DFT of the four-ste
 hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc* frames,
                           const UttDesc* utts, int n_utt, int maxL, float* out,
                           double* out_f64, int decimals, hipStream_t s);
+// One utterance of a reverb batch (fdlp_reverb): samples at pcm[off, off+T), y at [yoff, yoff+T+R-1).
+struct RevUtt {
+  int64_t off, T, yoff, noff;  // noff < 0: no noise mixing
+  double alpha;
+};
+hipError_t launch_reverb(const RevUtt* U, int n_utt, int64_t maxT, const void* pcm, int kind, int pre,
+                         const int16_t* noise, const double* rir, int R, double* x, double* y, double* xs,
+                         double* out, int64_t* out_len, hipStream_t s);
 int cmvn_chunks(int64_t rows);
 hipError_t launch_cmvn(const float* x, int64_t rows, int D, double* part, double* stats, hipStream_t s);
 }  // namespace fdlp

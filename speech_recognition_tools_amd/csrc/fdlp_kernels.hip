@@ -1926,4 +1926,162 @@ hipError_t launch_cmvn(const float* x, int64_t rows, int D, double* part, double
   return hipGetLastError();
 }
 
+// -----------------------------------------------------------------------------------------
+// 9. addReverb (features.py:110-115) after the optional diff / noise preprocessing
+//    (computeFDLPSpectrogram.py:160-170), per utterance u of T samples and an RIR of R taps:
+//      x = s | convolve(s, diff13, 'same') | s + alpha * noise[off:off+T]        (rev_pre_kernel)
+//      y = convolve(x, rir), length T+R-1                                       (rev_conv_kernel)
+//      xs[sh] = sum_n x[n] y[n+sh], sh < R  (np.correlate(x, y, 'valid') reversed) (rev_xcorr_kernel)
+//      sh* = the LARGEST shift attaining max xs (numpy's first argmax over the reversed order),
+//      out = y[sh*+1 : sh*+1+T] (shorter than T only when sh* = R-1)           (rev_select_kernel)
+//    fp64 direct sums (numpy's convolve/correlate are direct too).  VALU, 4 outputs per thread.
+// -----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rev_pre_kernel(const RevUtt* __restrict__ U, const void* __restrict__ pcm,
+                                                      int kind, int pre, const int16_t* __restrict__ noise,
+                                                      double* __restrict__ x) {
+  const RevUtt u = U[blockIdx.y];
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= u.T) return;
+  double v;
+  if (kind == 1) {
+    v = ((const double*)pcm)[u.off + t];
+  } else if (pre == 1) {  // scipy.signal.convolve(int16 s, diff kernel, 'same') -> int64, exact
+    const int16_t* s = (const int16_t*)pcm + u.off;
+    long long acc = 0;
+#pragma unroll
+    for (int q = 0; q < 13; ++q) {
+      const int64_t idx = t + 6 - q;
+      if (idx >= 0 && idx < u.T) acc += (long long)kDiffTaps[q] * (long long)s[idx];
+    }
+    v = (double)acc;
+  } else {
+    v = (double)((const int16_t*)pcm)[u.off + t];
+    if (u.noff >= 0) v = __dadd_rn(v, __dmul_rn(u.alpha, (double)noise[u.noff + t]));  // features.py:31
+  }
+  x[u.off + t] = v;
+}
+
+constexpr int kRevTile = 256;
+
+__global__ __launch_bounds__(256) void rev_conv_kernel(const RevUtt* __restrict__ U, const double* __restrict__ x,
+                                                       const double* __restrict__ rir, int R, double* __restrict__ y) {
+  __shared__ double rs[kRevTile];
+  __shared__ double xw[4 * 256 + kRevTile];
+  const RevUtt u = U[blockIdx.y];
+  const int64_t ny = u.T + R - 1;
+  const int64_t n0 = (int64_t)blockIdx.x * 1024;
+  if (n0 >= ny) return;
+  const int t4 = 4 * threadIdx.x;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  for (int k0 = 0; k0 < R; k0 += kRevTile) {
+    __syncthreads();
+    rs[threadIdx.x] = k0 + (int)threadIdx.x < R ? rir[k0 + threadIdx.x] : 0.0;
+    // xw[i] = x[n0 - k0 - (kRevTile-1) + i]
+    for (int i = threadIdx.x; i < 4 * 256 + kRevTile; i += 256) {
+      const int64_t q = n0 - k0 - (kRevTile - 1) + i;
+      xw[i] = (q >= 0 && q < u.T) ? x[u.off + q] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int kk = 0; kk < kRevTile; ++kk) {
+      const double r = rs[kk];
+      const int b = t4 + (kRevTile - 1) - kk;  // x[n - k] for n = n0 + t4, k = k0 + kk
+      a0 = fma(r, xw[b], a0);
+      a1 = fma(r, xw[b + 1], a1);
+      a2 = fma(r, xw[b + 2], a2);
+      a3 = fma(r, xw[b + 3], a3);
+    }
+  }
+  double* yo = y + u.yoff;
+  const int64_t n = n0 + t4;
+  if (n < ny) yo[n] = a0;
+  if (n + 1 < ny) yo[n + 1] = a1;
+  if (n + 2 < ny) yo[n + 2] = a2;
+  if (n + 3 < ny) yo[n + 3] = a3;
+}
+
+__global__ __launch_bounds__(256) void rev_xcorr_kernel(const RevUtt* __restrict__ U, const double* __restrict__ x,
+                                                        const double* __restrict__ y, int R, double* __restrict__ xs) {
+  __shared__ double xt[kRevTile];
+  __shared__ double yw[4 * 256 + kRevTile];
+  const RevUtt u = U[blockIdx.y];
+  const int s0 = blockIdx.x * 1024;
+  if (s0 >= R) return;
+  const int64_t ny = u.T + R - 1;
+  const int t4 = 4 * threadIdx.x;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  for (int64_t m0 = 0; m0 < u.T; m0 += kRevTile) {
+    __syncthreads();
+    xt[threadIdx.x] = m0 + threadIdx.x < u.T ? x[u.off + m0 + threadIdx.x] : 0.0;
+    // yw[i] = y[m0 + s0 + i]
+    for (int i = threadIdx.x; i < 4 * 256 + kRevTile; i += 256) {
+      const int64_t q = m0 + s0 + i;
+      yw[i] = q < ny ? y[u.yoff + q] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int mm = 0; mm < kRevTile; ++mm) {
+      const double xv = xt[mm];
+      const int b = mm + t4;  // y[m + sh] for m = m0 + mm, sh = s0 + t4
+      a0 = fma(xv, yw[b], a0);
+      a1 = fma(xv, yw[b + 1], a1);
+      a2 = fma(xv, yw[b + 2], a2);
+      a3 = fma(xv, yw[b + 3], a3);
+    }
+  }
+  double* o = xs + (int64_t)blockIdx.y * R;
+  const int sh = s0 + t4;
+  if (sh < R) o[sh] = a0;
+  if (sh + 1 < R) o[sh + 1] = a1;
+  if (sh + 2 < R) o[sh + 2] = a2;
+  if (sh + 3 < R) o[sh + 3] = a3;
+}
+
+__global__ __launch_bounds__(256) void rev_select_kernel(const RevUtt* __restrict__ U, const double* __restrict__ y,
+                                                         const double* __restrict__ xs, int R,
+                                                         double* __restrict__ out, int64_t* __restrict__ out_len) {
+  __shared__ double bv[256];
+  __shared__ int bs[256];
+  const RevUtt u = U[blockIdx.x];
+  const double* o = xs + (int64_t)blockIdx.x * R;
+  double best = -INFINITY;
+  int bsh = -1;
+  for (int sh = threadIdx.x; sh < R; sh += 256) {
+    const double v = o[sh];
+    if (v > best || (v == best && sh > bsh) || bsh < 0) { best = v; bsh = sh; }
+  }
+  bv[threadIdx.x] = best;
+  bs[threadIdx.x] = bsh;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const double v2 = bv[threadIdx.x + w];
+      const int s2 = bs[threadIdx.x + w];
+      if (s2 >= 0 && (bs[threadIdx.x] < 0 || v2 > bv[threadIdx.x] || (v2 == bv[threadIdx.x] && s2 > bs[threadIdx.x]))) {
+        bv[threadIdx.x] = v2;
+        bs[threadIdx.x] = s2;
+      }
+    }
+    __syncthreads();
+  }
+  const int64_t ind = (int64_t)bs[0] + 1;  // indM = R - argmax
+  const int64_t ny = u.T + R - 1;
+  const int64_t L = min(u.T, ny - ind);
+  for (int64_t t = threadIdx.x; t < L; t += 256) out[u.off + t] = y[u.yoff + ind + t];
+  if (threadIdx.x == 0) out_len[blockIdx.x] = L;
+}
+
+hipError_t launch_reverb(const RevUtt* U, int n_utt, int64_t maxT, const void* pcm, int kind, int pre,
+                         const int16_t* noise, const double* rir, int R, double* x, double* y, double* xs,
+                         double* out, int64_t* out_len, hipStream_t s) {
+  if (n_utt <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rev_pre_kernel, dim3((unsigned)((maxT + 255) / 256), n_utt), dim3(256), 0, s, U, pcm, kind,
+                     pre, noise, x);
+  hipLaunchKernelGGL(rev_conv_kernel, dim3((unsigned)((maxT + R - 1 + 1023) / 1024), n_utt), dim3(256), 0, s, U, x,
+                     rir, R, y);
+  hipLaunchKernelGGL(rev_xcorr_kernel, dim3((unsigned)((R + 1023) / 1024), n_utt), dim3(256), 0, s, U, x, y, R, xs);
+  hipLaunchKernelGGL(rev_select_kernel, dim3(n_utt), dim3(256), 0, s, U, y, xs, R, out, out_len);
+  return hipGetLastError();
+}
+
 }  // namespace fdlp

@@ -858,6 +858,47 @@ int fdlp_cepstrum_rows(fdlp_plan* p, const double* a, const double* gg, int32_t 
   return FDLP_OK;
 }
 
+int fdlp_reverb(const fdlp_reverb_batch* b, void* stream) {
+  if (!b || b->n_utt < 0 || !b->pcm_off || !b->utt_len || !b->rir_dev || b->rir_len < 1 || !b->out_dev ||
+      !b->out_len || (b->n_utt > 0 && !b->pcm_dev) || (b->noise_dev && (!b->noise_off || !b->noise_alpha)) ||
+      (b->pcm_kind != FDLP_PCM_I16 && b->pcm_kind != FDLP_PCM_F64) ||
+      (b->pcm_kind == FDLP_PCM_F64 && (b->noise_dev || b->preprocess != FDLP_PRE_NONE)))
+    return fail(FDLP_E_INVALID, "fdlp_reverb: bad args");
+  if (b->n_utt == 0) return FDLP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int R = b->rir_len;
+  std::vector<fdlp::RevUtt> U(b->n_utt);
+  int64_t extent = 0, ny = 0, maxT = 0;
+  for (int i = 0; i < b->n_utt; ++i) {
+    const int64_t T = b->utt_len[i];
+    if (T < 1 || b->pcm_off[i] < 0) return fail(FDLP_E_INVALID, "fdlp_reverb: empty utterance");
+    U[i].off = b->pcm_off[i];
+    U[i].T = T;
+    U[i].yoff = ny;
+    U[i].noff = b->noise_dev ? b->noise_off[i] : -1;
+    U[i].alpha = b->noise_dev ? b->noise_alpha[i] : 0.0;
+    ny += T + R - 1;
+    extent = std::max(extent, b->pcm_off[i] + T);
+    maxT = std::max(maxT, T);
+  }
+  fdlp::RevUtt* dU = nullptr;
+  double *x = nullptr, *y = nullptr, *xs = nullptr;
+  int64_t* dlen = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&dU, sizeof(fdlp::RevUtt) * U.size(), s));
+  HIP_TRY(hipMallocAsync((void**)&x, sizeof(double) * extent, s));
+  HIP_TRY(hipMallocAsync((void**)&y, sizeof(double) * ny, s));
+  HIP_TRY(hipMallocAsync((void**)&xs, sizeof(double) * (size_t)b->n_utt * R, s));
+  HIP_TRY(hipMallocAsync((void**)&dlen, sizeof(int64_t) * b->n_utt, s));
+  HIP_TRY(hipMemcpyAsync(dU, U.data(), sizeof(fdlp::RevUtt) * U.size(), hipMemcpyHostToDevice, s));
+  const int pre = b->preprocess == FDLP_PRE_DIFF ? 1 : 0;
+  HIP_TRY(fdlp::launch_reverb(dU, b->n_utt, maxT, b->pcm_dev, b->pcm_kind, pre, b->noise_dev, b->rir_dev, R, x, y,
+                              xs, b->out_dev, dlen, s));
+  HIP_TRY(hipMemcpyAsync(b->out_len, dlen, sizeof(int64_t) * b->n_utt, hipMemcpyDeviceToHost, s));
+  for (void* d : {(void*)dU, (void*)x, (void*)y, (void*)xs, (void*)dlen}) HIP_TRY(hipFreeAsync(d, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return FDLP_OK;
+}
+
 int fdlp_cmvn_accumulate(const float* feats, int64_t rows, int32_t dim, double* stats, void* stream) {
   if (rows < 0 || dim <= 0 || !stats || (rows > 0 && !feats)) return fail(FDLP_E_INVALID, "fdlp_cmvn_accumulate: bad args");
   hipStream_t s = (hipStream_t)stream;

@@ -99,14 +99,13 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
             noise_info = add_noise.strip().split(',')
             noise = load_noise(noise_info[0])
             snr = float(noise_info[1])
+    rir = None
     if add_reverb:                                                          # :75-91
         if add_reverb == 'clean':
             print('%s: No reverberation added!' % sys.argv[0])
-        elif add_reverb in ('small_room', 'medium_room', 'large_room'):
-            raise NotImplementedError("--add_reverb %s (RIR convolution, features.py:110-115) is not ported yet"
-                                      % add_reverb)
         else:
-            raise ValueError('Invalid type of reverberation!')
+            from speech_recognition_tools_amd.augment import load_rir
+            rir = load_rir(add_reverb)                                      # ValueError for unknown rooms
     if not args.gamma_weight.strip().split(',')[0] == "None":
         print('%s: Adding gamma filter on modulation frequencies...' % sys.argv[0])
     if scp_type not in ('wav', 'segment'):
@@ -118,6 +117,7 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
     jit_rng = PyRandom(args.seed)
     noise_rng = NpRandom(args.noise_seed) if noise is not None else None
     noise_dev = torch.from_numpy(np.ascontiguousarray(noise)).cuda(device) if noise is not None else None
+    rir_dev = torch.from_numpy(np.ascontiguousarray(rir, dtype=np.float64)).cuda(device) if rir is not None else None
     cmvn = None
     if args.cmvn_stats:  # fused e2e/*/run_fdlp_e1.sh `compute-cmvn-stats` (speech_recognition_tools_amd.cmvn)
         from speech_recognition_tools_amd.cmvn import CmvnAccumulator
@@ -149,14 +149,21 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
         if not pending:
             return
         lens = [x[1].shape[0] for x in pending]
-        jit = np.concatenate([jit_rng.randbits2(x[2] - 1) for x in pending])
         pcm_host = torch.from_numpy(np.concatenate([x[1] for x in pending])).pin_memory()
         pcm = pcm_host.to(torch.device("cuda", device), non_blocking=True)
         kw = {}
         if noise is not None:
             kw = dict(noise=noise_dev, noise_off=[x[3] for x in pending], noise_alpha=[x[4] for x in pending])
-        out, rows, _ = plan.compute(pcm, lens, jit, ark_decimals=args.ark_precision,
-                                    preprocess="diff" if diff else None, **kw)
+        pre = "diff" if diff else None
+        offs = None
+        if rir_dev is not None:  # :168-170 on the device; lengths can shrink by one (edge case)
+            from speech_recognition_tools_amd.augment import reverb
+            offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+            pcm, lens = reverb(pcm, lens, rir_dev, offsets=offs, preprocess=pre, **kw)
+            kw, pre = {}, None
+        jit = np.concatenate([jit_rng.randbits2(plan.geometry(int(T))[0] - 1) for T in lens])
+        out, rows, _ = plan.compute(pcm, lens, jit, offsets=offs, ark_decimals=args.ark_precision,
+                                    preprocess=pre, **kw)
         if cmvn is not None:
             cmvn.add(out[:int(rows[-1])])
         host = torch.empty(out.shape, dtype=out.dtype, pin_memory=True)

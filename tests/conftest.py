@@ -24,7 +24,8 @@ def load_golden(name):
     return meta, sig, ref, z
 
 
-GOLDEN_SETS = ["wsj", "reverb", "chime4_noise", "cli_default_mel", "mel80", "wsj_diff", "gamma_lifter_odd"]
+GOLDEN_SETS = ["wsj", "reverb", "chime4_noise", "cli_default_mel", "mel80", "wsj_diff", "gamma_lifter_odd",
+               "reverb_rir", "reverb_rir_noise"]
 
 
 def oracle_cfg(meta):

@@ -63,7 +63,17 @@ def pesq_clip(name, seconds):
     return y[: int(seconds * 16000)]
 
 
-def run_reference(signals, opts, seed, noise_seed=None, noise=None, noise_name=None):
+def synthetic_rir(R, seed, t60=0.25):
+    """Stereo int16 RIR: a direct path + exponentially decaying noise tail (channel 1 is the one used)."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(R) / 16000.0
+    h = rng.standard_normal((R, 2)) * np.exp(-6.9 * t / t60)[:, None] * 0.3
+    h[0] = [0.9, 0.8]
+    h[37] += [0.4, -0.35]
+    return np.clip(np.round(h * 32767), -32768, 32767).astype(np.int16)
+
+
+def run_reference(signals, opts, seed, noise_seed=None, noise=None, noise_name=None, rir=None):
     """Write WAVs + scp, call getFeats with an argparse Namespace, capture the dict."""
     sys.path.insert(0, os.path.join(REF, "src/featgen"))
     import computeFDLPSpectrogram as cf  # noqa: E402
@@ -85,6 +95,9 @@ def run_reference(signals, opts, seed, noise_seed=None, noise=None, noise_name=N
         if noise is not None:
             os.makedirs(os.path.join(td, "noises"), exist_ok=True)
             wavfile.write(os.path.join(td, "noises", noise_name + ".wav"), 16000, noise)
+        if rir is not None:  # computeFDLPSpectrogram.py:76: ./RIR/RIR_SmallRoom1_near_AnglA.wav
+            os.makedirs(os.path.join(td, "RIR"), exist_ok=True)
+            wavfile.write(os.path.join(td, "RIR", "RIR_SmallRoom1_near_AnglA.wav"), 16000, rir)
         os.chdir(td)
         try:
             ns = argparse.Namespace(
@@ -175,9 +188,28 @@ def cli_options_fixture():
     print("wrote cli_options.json", len(opts))
 
 
+def reverb_rir_fixture():
+    """--add_reverb small_room (features.py:110-115) with a synthetic stereo RIR, clean and with noise."""
+    rir = synthetic_rir(4000, 5)
+    sig = OrderedDict()
+    sig["v1p2"] = speech_like(19200, 51)
+    sig["v3p0"] = speech_like(48000, 52)
+    sig["vwhite"] = white(30000, 53)
+    opts = dict(WSJ, add_reverb="small_room")
+    save("reverb_rir", sig, opts, 99, run_reference(sig, opts, 99, rir=rir), more={"rir": rir})
+    noise = white(16000 * 6, 54, scale=1500.0)
+    opts_n = dict(CHIME4, add_reverb="small_room", add_noise="babble,20")
+    save("reverb_rir_noise", sig, opts_n, 98,
+         run_reference(sig, opts_n, 98, noise_seed=4, noise=noise, noise_name="babble", rir=rir),
+         extra=dict(noise_seed=4), more={"rir": rir, "noise_babble": noise})
+
+
 def main():
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
     sys.dont_write_bytecode = True
+    if "--reverb-only" in sys.argv:
+        reverb_rir_fixture()
+        return
     cli_options_fixture()
     if "--cli-only" in sys.argv:
         return
@@ -241,6 +273,7 @@ def main():
     opts = dict(opts, lifter_config=None)
     save("gamma_lifter_odd", gw, opts, 13, feats, extra=dict(lifter=lif.tolist()))
     os.unlink(lifpath)
+    reverb_rir_fixture()
 
 
 if __name__ == "__main__":

@@ -146,3 +146,24 @@ def test_driver_script_two_jobs(tmp_path):
     want = CO.global_stats(arks[u] for u in meta["utts"])
     assert got[0, -1] == want[0, -1]
     assert np.max(np.abs(got - want) / np.maximum(np.abs(want), 1.0)) <= 1e-12
+
+
+@pytest.mark.parametrize("name", ["reverb_rir", "reverb_rir_noise"])
+def test_cli_add_reverb(tmp_path, monkeypatch, name):
+    """--add_reverb small_room reads ./RIR/RIR_SmallRoom1_near_AnglA.wav (channel 1 / 2^15) and
+    convolves + re-aligns on the device (after the noise mixing when both are given)."""
+    from speech_recognition_tools_amd.featgen.computeFDLPSpectrogram import getFeats
+    meta, sig, ref, z = load_golden(name)
+    d = tmp_path / "r"
+    (d / "RIR").mkdir(parents=True)
+    wavfile.write(str(d / "RIR" / "RIR_SmallRoom1_near_AnglA.wav"), 16000, z["rir"])
+    extra = ["--add_reverb=small_room"]
+    if "noise_babble" in z.files:
+        (d / "noises").mkdir()
+        wavfile.write(str(d / "noises" / "babble.wav"), 16000, z["noise_babble"])
+        extra += ["--add_noise=" + meta["opts"]["add_noise"], "--noise_seed=%d" % meta["extra"]["noise_seed"]]
+    scp = _write_scp(str(d), sig, meta["utts"])
+    monkeypatch.chdir(str(d))
+    out = str(d / "rv")
+    getFeats(_args([scp, out] + _opts(meta) + extra))
+    _check(out, meta, ref, meta["utts"])

@@ -51,10 +51,17 @@ def run_gpu(meta, sig, z, support_eps=None, max_frames=256, debug=False, path="a
         plan.set_debug(True)
     utts = meta["utts"]
     lens = [sig[u].size for u in utts]
-    nj = sum(max(plan.geometry(T)[0] - 1, 0) for T in lens)
-    jit = PyRandom(meta["seed"]).randbits2(nj)
     pcm, kw = _batch_inputs(meta, sig, z)
-    out, rows, out64 = plan.compute(torch.from_numpy(pcm).cuda(), lens, jit, want_f64=True, **kw)
+    pcm = torch.from_numpy(pcm).cuda()
+    if meta["opts"].get("add_reverb", "clean") != "clean":  # addReverb on the device (fdlp_reverb)
+        from oracle import fdlp_oracle as O
+        from speech_recognition_tools_amd.augment import reverb
+        rir = torch.from_numpy(O.load_rir(z["rir"])).cuda()
+        pcm, lens = reverb(pcm, lens, rir, **kw)
+        kw = {}
+    nj = sum(max(plan.geometry(int(T))[0] - 1, 0) for T in lens)
+    jit = PyRandom(meta["seed"]).randbits2(nj)
+    out, rows, out64 = plan.compute(pcm, lens, jit, want_f64=True, **kw)
     torch.cuda.synchronize()
     out, out64 = out.cpu().numpy(), out64.cpu().numpy()
     res = {u: (out64[rows[i]:rows[i + 1]], out[rows[i]:rows[i + 1]]) for i, u in enumerate(utts)}
@@ -232,3 +239,27 @@ def test_lattice_durbin_matches_lds_durbin(name, monkeypatch):
         # amplifies that in the near-empty 4-8 kHz bands of the upsampled PESQ clips (1.4e-8 measured)
         # and in the degenerate short2 (its own tolerance).  Both stay within TOL of the reference.
         assert np.abs(a[fin] - b[fin]).max() <= TOL_UTT.get(u, 1e-6), (name, u)
+
+
+def test_reverb_kernel_vs_oracle():
+    """fdlp_reverb (preprocessing + full convolution + xcorr argmax alignment) against the oracle's
+    restatement of addReverb (features.py:110-115) on random int16 signals, with and without the diff
+    preprocessing, including an RIR longer than one kernel tile and an utterance shorter than the RIR."""
+    from oracle import fdlp_oracle as O
+    from speech_recognition_tools_amd.augment import reverb
+    rng = np.random.default_rng(3)
+    rir = np.concatenate([[0.7, 0.0, -0.2], rng.standard_normal(1500) * np.exp(-np.arange(1500) / 300.0) * 0.2])
+    sigs = [np.clip(rng.standard_normal(T) * 2000, -32768, 32767).astype(np.int16) for T in (5000, 1200, 777, 17000)]
+    lens = [s.size for s in sigs]
+    pcm = torch.from_numpy(np.concatenate(sigs)).cuda()
+    for pre in (None, "diff"):
+        out, ol = reverb(pcm, lens, torch.from_numpy(rir).cuda(), preprocess=pre)
+        out = out.cpu().numpy()
+        off = 0
+        for s, T, L in zip(sigs, lens, ol):
+            x = O.diff_signal(s) if pre == "diff" else s
+            ref = O.add_reverb(x, rir)
+            assert L == ref.size
+            got = out[off:off + L]
+            assert np.abs(got - ref).max() <= 1e-9 * max(1.0, np.abs(ref).max())
+            off += T
