@@ -174,6 +174,30 @@ int fdlp_lpc_rows(fdlp_plan* plan, const double* band_dev, int32_t n_items, doub
 int fdlp_cepstrum_rows(fdlp_plan* plan, const double* a_dev, const double* gg_dev,
                        int32_t n_items, int32_t p, int32_t lim, double* cep_dev, void* stream);
 
+/* ---- sibling feature: mel spectrum (src/featgen/computeMelSpectrum.py, run_melspec) ----- */
+/* Replaces compute_mel_spectrum (computeMelSpectrum.py:40-170): getFrames with np.hamming(L),
+ * |scipy.fftpack.fft(frame, nfft)[:nfft/2+1]| @ fbank.T, log10 ('log') or squared ('power'). */
+typedef struct fdlp_mel_config {
+  int32_t nfilters;          /* --nfilters (23)                                        (:26)   */
+  int32_t nfft;              /* --nfft (1024); even, nfft/2 a 2/3/5/7-smooth size <= 2048 (:29) */
+  int32_t frate;             /* --frate (100)                                          (:28)   */
+  int32_t srate;             /* 16000                                                  (:40)   */
+  int32_t fbank_kind;        /* --fbank_type "mel,wf" | "cochlear,om_w,alp,fixed,bet,wf" (:53-67) */
+  int32_t fixed;
+  int32_t power;             /* --spectrum_type: 0 log (log10), 1 power (squared)      (:150-158) */
+  double fduration;          /* --fduration (0.02)                                     (:27)   */
+  double warp_fact, om_w, alp, bet;
+  int32_t max_frames;        /* frames per fdlp_mel_compute call                             */
+} fdlp_mel_config;
+typedef struct fdlp_mel_plan fdlp_mel_plan;
+int fdlp_mel_plan_create(const fdlp_mel_config* cfg, int device, fdlp_mel_plan** out);
+int fdlp_mel_plan_destroy(fdlp_mel_plan* plan);
+/* F frames of an utterance of T samples (getFrames, features.py:151). */
+int fdlp_mel_geometry(const fdlp_mel_plan* plan, int64_t T, int32_t* F);
+/* A batch (fdlp_batch: pcm, offsets, lengths, noise / diff preprocessing, out [sum F, nfilters] at
+ * out_row, optional fp64 copy, ark_decimals; `jitter` is unused). */
+int fdlp_mel_compute(fdlp_mel_plan* plan, const fdlp_batch* batch, void* stream);
+
 /* ---- augmentation: addReverb (features.py:110-115) -------------------------------------- */
 /* --add_reverb small_room|medium_room|large_room (computeFDLPSpectrogram.py:75-91, :168-170): after the
  * optional diff / noise preprocessing, every utterance is convolved with the RIR (channel 1 of

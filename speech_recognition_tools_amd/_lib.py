@@ -60,6 +60,14 @@ class FdlpBatchC(ctypes.Structure):
     ]
 
 
+class FdlpMelConfigC(ctypes.Structure):
+    _fields_ = [
+        ("nfilters", c_i32), ("nfft", c_i32), ("frate", c_i32), ("srate", c_i32), ("fbank_kind", c_i32),
+        ("fixed", c_i32), ("power", c_i32), ("fduration", c_dbl), ("warp_fact", c_dbl), ("om_w", c_dbl),
+        ("alp", c_dbl), ("bet", c_dbl), ("max_frames", c_i32),
+    ]
+
+
 class FdlpReverbBatchC(ctypes.Structure):
     _fields_ = [
         ("n_utt", c_i32), ("pcm_kind", c_i32), ("pcm_dev", c_p), ("pcm_off", P_i64), ("utt_len", P_i64),
@@ -105,6 +113,10 @@ SIGNATURES = {
     "fdlp_ark_close": (c_i32, [c_p]),
     "fdlp_cmvn_accumulate": (c_i32, [c_p, c_i64, c_i32, c_p, c_p]),
     "fdlp_reverb": (c_i32, [ctypes.POINTER(FdlpReverbBatchC), c_p]),
+    "fdlp_mel_plan_create": (c_i32, [ctypes.POINTER(FdlpMelConfigC), c_i32, ctypes.POINTER(c_p)]),
+    "fdlp_mel_plan_destroy": (c_i32, [c_p]),
+    "fdlp_mel_geometry": (c_i32, [c_p, c_i64, P_i32]),
+    "fdlp_mel_compute": (c_i32, [c_p, ctypes.POINTER(FdlpBatchC), c_p]),
     "fdlp_mat_reader_open": (c_i32, [ctypes.c_char_p, ctypes.POINTER(c_p)]),
     "fdlp_mat_reader_next": (c_i32, [c_p, ctypes.POINTER(ctypes.c_char_p), P_i32, P_i32,
                                      ctypes.POINTER(ctypes.POINTER(ctypes.c_float))]),

@@ -104,6 +104,27 @@ constexpr int kDftMaxSub = 512;  // longest LDS-resident sub-DFT of the four-ste
 hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc* frames,
                           const UttDesc* utts, int n_utt, int maxL, float* out,
                           double* out_f64, int decimals, hipStream_t s);
+// Mel spectrum (computeMelSpectrum.py): one analysis frame and the plan constants.
+struct MelFrame {
+  int64_t pcm_off, noise_off;  // noise_off < 0: no mixing
+  double alpha;
+  int64_t out_row;
+  int32_t T, k;
+};
+struct MelConsts {
+  int L, hop, ext, nfft, nh, nbins, nfilters, power;
+  const double* window;  // [L]  np.hamming(L)
+  const double* fbank;   // [nfilters, nbins]
+  const int* lo;         // [nfilters] first non-zero tap
+  const int* hi;         // [nfilters] one past the last non-zero tap
+  const double2* om;     // [nh] exp(-2 pi i q / nh)
+  const double2* rtw;    // [nh + 1] exp(-2 pi i k / nfft)
+  DftPlan dp;            // length nh
+};
+hipError_t launch_mel(const MelConsts& c, const MelFrame* frames, int nframes, const void* pcm, int pcm_kind,
+                      const int16_t* noise, float* out, double* out64, int decimals, hipStream_t s);
+size_t mel_lds_bytes(int nh);
+
 // One utterance of a reverb batch (fdlp_reverb): samples at pcm[off, off+T), y at [yoff, yoff+T+R-1).
 struct RevUtt {
   int64_t off, T, yoff, noff;  // noff < 0: no noise mixing

@@ -2084,4 +2084,103 @@ hipError_t launch_reverb(const RevUtt* U, int n_utt, int64_t maxT, const void* p
   return hipGetLastError();
 }
 
+// -----------------------------------------------------------------------------------------
+// 10. Mel spectrum (src/featgen/computeMelSpectrum.py:147-158, the run_melspec baseline feature):
+//     frame = reflect-padded x[k*hop + i - ext] * hamming(L)[i] (getFrames, features.py:118-154),
+//     |scipy.fftpack.fft(frame, nfft)[:nfft/2+1]| @ fbank.T, then log10 (or squared for 'power').
+//     The real length-nfft FFT runs as a length-nfft/2 complex FFT of the packed frame (z[q] = x[2q] +
+//     i x[2q+1]) in LDS with the real-FFT unpacking; kMelCols frames per workgroup.
+// -----------------------------------------------------------------------------------------
+constexpr int kMelCols = 2;
+
+size_t mel_lds_bytes(int nh) { return sizeof(double2) * 2 * (size_t)nh * kMelCols; }
+
+__global__ __launch_bounds__(256) void mel_kernel(MelConsts c, const MelFrame* __restrict__ frames, int nframes,
+                                                  const void* __restrict__ pcm, int pcm_kind,
+                                                  const int16_t* __restrict__ noise, float* __restrict__ out,
+                                                  double* __restrict__ out64, int decimals, double scale10) {
+  extern __shared__ double2 mel_sh[];
+  double2* a = mel_sh;
+  double2* b = mel_sh + (size_t)c.nh * kMelCols;
+  const int f0 = blockIdx.x * kMelCols;
+  const int nh = c.nh;
+  const int Luse = c.L < c.nfft ? c.L : c.nfft;  // fft(x, n) truncates a longer frame
+  // 1. packed windowed frames: a[q * kMelCols + col] = x[2q] + i x[2q+1]
+  for (int e = threadIdx.x; e < nh * kMelCols; e += blockDim.x) {
+    const int col = e % kMelCols, q = e / kMelCols;
+    const int f = f0 + col;
+    double v[2] = {0.0, 0.0};
+    if (f < nframes) {
+      const MelFrame fd = frames[f];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int i = 2 * q + h;
+        if (i < Luse) {
+          const int64_t t = reflect_idx((int64_t)fd.k * c.hop + i - c.ext, fd.T);
+          double sv;
+          if (pcm_kind == 0) {
+            sv = (double)((const int16_t*)pcm)[fd.pcm_off + t];
+            if (fd.noise_off >= 0) sv = __dadd_rn(sv, __dmul_rn(fd.alpha, (double)noise[fd.noise_off + t]));
+          } else if (pcm_kind == 1) {
+            sv = ((const double*)pcm)[fd.pcm_off + t];
+          } else {  // convolve(int16 s, diff kernel, 'same') -> int64 (computeMelSpectrum.py:136-139)
+            const int16_t* x = (const int16_t*)pcm + fd.pcm_off;
+            long long acc = 0;
+#pragma unroll
+            for (int qq = 0; qq < 13; ++qq) {
+              const int64_t idx = t + 6 - qq;
+              if (idx >= 0 && idx < fd.T) acc += (long long)kDiffTaps[qq] * (long long)x[idx];
+            }
+            sv = (double)acc;
+          }
+          v[h] = __dmul_rn(sv, c.window[i]);
+        }
+      }
+    }
+    a[e] = make_double2(v[0], v[1]);
+  }
+  __syncthreads();
+  double2* Z = lds_dft(a, b, c.om, c.dp, kMelCols);
+  double* mag = (double*)(Z == a ? b : a);  // [kMelCols][nbins]
+  // 2. real-FFT unpacking: X[k] = E[k] + W^k O[k], E = (Z[k] + conj Z[nh-k]) / 2, O = (Z[k] - conj Z[nh-k]) / 2i
+  for (int e = threadIdx.x; e < c.nbins * kMelCols; e += blockDim.x) {
+    const int col = e % kMelCols, k = e / kMelCols;
+    const double2 zk = Z[(k % nh) * kMelCols + col];
+    const double2 zc = Z[((nh - k) % nh) * kMelCols + col];
+    const double2 E = make_double2(0.5 * (zk.x + zc.x), 0.5 * (zk.y - zc.y));
+    const double2 O = make_double2(0.5 * (zk.y + zc.y), -0.5 * (zk.x - zc.x));
+    const double2 w = c.rtw[k];
+    const double2 X = make_double2(E.x + (w.x * O.x - w.y * O.y), E.y + (w.x * O.y + w.y * O.x));
+    mag[col * c.nbins + k] = hypot(X.x, X.y);
+  }
+  __syncthreads();
+  // 3. filterbank projection + log10 / power (computeMelSpectrum.py:150-158)
+  for (int e = threadIdx.x; e < c.nfilters * kMelCols; e += blockDim.x) {
+    const int col = e / c.nfilters, m = e % c.nfilters;
+    const int f = f0 + col;
+    if (f >= nframes) continue;
+    const double* w = c.fbank + (size_t)m * c.nbins;
+    const double* mg = mag + col * c.nbins;
+    double acc = 0.0;
+    for (int k = c.lo[m]; k < c.hi[m]; ++k) acc = fma(mg[k], w[k], acc);
+    const double v = c.power ? acc * acc : log10(acc);
+    const int64_t o = frames[f].out_row * c.nfilters + m;
+    if (out64) out64[o] = v;
+    if (out) out[o] = decimals >= 0 ? (float)(nearbyint(v * scale10) / scale10) : (float)v;
+  }
+}
+
+hipError_t launch_mel(const MelConsts& c, const MelFrame* frames, int nframes, const void* pcm, int pcm_kind,
+                      const int16_t* noise, float* out, double* out64, int decimals, hipStream_t s) {
+  if (nframes <= 0) return hipSuccess;
+  double scale10 = 1.0;
+  for (int i = 0; i < decimals; ++i) scale10 *= 10.0;
+  const size_t lds = mel_lds_bytes(c.nh);
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)mel_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(mel_kernel, dim3((nframes + kMelCols - 1) / kMelCols), dim3(256), lds, s, c, frames, nframes,
+                     pcm, pcm_kind, noise, out, out64, decimals, scale10);
+  return hipGetLastError();
+}
+
 }  // namespace fdlp

@@ -858,6 +858,166 @@ int fdlp_cepstrum_rows(fdlp_plan* p, const double* a, const double* gg, int32_t 
   return FDLP_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// mel spectrum plan (computeMelSpectrum.py:40-170)
+// ---------------------------------------------------------------------------------------------
+struct fdlp_mel_plan {
+  fdlp_mel_config cfg{};
+  int device = 0;
+  int L = 0, hop = 0, sp_b = 0, sp_f = 0, ext = 0, nbins = 0;
+  fdlp::MelConsts mc{};
+  double *d_win = nullptr, *d_fb = nullptr;
+  int *d_lo = nullptr, *d_hi = nullptr;
+  double2 *d_om = nullptr, *d_rtw = nullptr;
+  fdlp::MelFrame* d_frames = nullptr;
+  fdlp::MelFrame* h_frames = nullptr;  // pinned staging
+  hipEvent_t staging_done = nullptr;
+  bool staging_pending = false;
+};
+
+static int free_mel_plan(fdlp_mel_plan* p) {
+  if (!p) return FDLP_OK;
+  void* devs[] = {p->d_win, p->d_fb, p->d_lo, p->d_hi, p->d_om, p->d_rtw, p->d_frames};
+  for (void* d : devs)
+    if (d) (void)hipFree(d);
+  if (p->h_frames) (void)hipHostFree(p->h_frames);
+  if (p->staging_done) (void)hipEventDestroy(p->staging_done);
+  delete p;
+  return FDLP_OK;
+}
+
+static int64_t mel_frames_of(const fdlp_mel_plan* p, int64_t T) {
+  const int64_t lim = T + 2 * (int64_t)p->ext - p->sp_b - p->sp_f;  // getFrames: k*hop < lim
+  if (lim <= 0) return 0;
+  return (lim - 1) / p->hop + 1;
+}
+
+int fdlp_mel_plan_create(const fdlp_mel_config* cfg, int device, fdlp_mel_plan** out) {
+  if (!cfg || !out) return fail(FDLP_E_INVALID, "fdlp_mel_plan_create: null argument");
+  *out = nullptr;
+  const fdlp_mel_config& c = *cfg;
+  if (c.nfilters < 1 || c.srate < 1 || c.frate < 1 || !(c.fduration > 0) || c.max_frames < 1)
+    return fail(FDLP_E_INVALID, "invalid mel configuration");
+  if (c.nfft < 2 || c.nfft % 2 || c.nfft / 2 > 2048) return fail(FDLP_E_INVALID, "nfft must be even and <= 4096");
+  auto* p = new (std::nothrow) fdlp_mel_plan;
+  if (!p) return fail(FDLP_E_NOMEM, "out of memory");
+  p->cfg = c;
+  p->device = device;
+  int rc;
+#define MEL_FAIL(code, msg) do { rc = fail(code, msg); free_mel_plan(p); return rc; } while (0)
+#define MEL_TRY(expr) do { rc = (expr); if (rc != FDLP_OK) { std::string m_ = fdlp::last_error_slot(); free_mel_plan(p); fdlp::last_error_slot() = m_; return rc; } } while (0)
+  p->L = (int)((double)c.srate * c.fduration);       // features.py:134
+  p->hop = (int)((double)c.srate / (double)c.frate);  // features.py:135
+  if (p->L % 2 == 0) { p->sp_b = p->L / 2 - 1; p->sp_f = p->L / 2; p->ext = p->L / 2 - 1; }
+  else { p->sp_b = p->sp_f = p->ext = (p->L - 1) / 2; }
+  if (p->L < 2 || p->hop < 1) MEL_FAIL(FDLP_E_INVALID, "frame length / hop too small");
+  const int nh = c.nfft / 2;
+  fdlp::DftPlan dp{};
+  if (!factor_radices(nh, &dp)) MEL_FAIL(FDLP_E_INVALID, "nfft/2 must factor into 2, 3, 5 and 7");
+  std::vector<double> fb;
+  int ncol = 0;
+  if (c.fbank_kind == FDLP_FBANK_MEL) fb = fbank_mel(c.nfilters, c.nfft, c.srate, c.warp_fact, &ncol);  // :57
+  else if (c.fbank_kind == FDLP_FBANK_COCHLEAR)
+    fb = fbank_cochlear(c.nfilters, c.nfft, c.srate, c.om_w, c.alp, c.fixed, c.bet, c.warp_fact, &ncol);  // :63-65
+  else MEL_FAIL(FDLP_E_INVALID, "Invalid type of filter bank, use mel or cochlear with proper configuration");
+  if (ncol != nh + 1) MEL_FAIL(FDLP_E_INVALID, "filterbank width does not match nfft/2+1");
+  p->nbins = ncol;
+  std::vector<int> lo(c.nfilters, 0), hi(c.nfilters, 0);
+  for (int m = 0; m < c.nfilters; ++m) {
+    int a = ncol, b = 0;
+    for (int k = 0; k < ncol; ++k)
+      if (fb[(size_t)m * ncol + k] != 0.0) { a = std::min(a, k); b = k + 1; }
+    if (b <= a) { a = 0; b = 0; }
+    lo[m] = a;
+    hi[m] = b;
+  }
+  const std::vector<double> win = cos_window(p->L, 0.54, 0.46);  // np.hamming (computeMelSpectrum.py:41)
+  const long double PI = 3.141592653589793238462643383279502884L;
+  std::vector<double2> om(nh), rtw(nh + 1);
+  for (int q = 0; q < nh; ++q) {
+    const long double ang = -2.0L * PI * (long double)q / (long double)nh;
+    om[q] = make_double2((double)cosl(ang), (double)sinl(ang));
+  }
+  for (int k = 0; k <= nh; ++k) {
+    const long double ang = -2.0L * PI * (long double)k / (long double)c.nfft;
+    rtw[k] = make_double2((double)cosl(ang), (double)sinl(ang));
+  }
+  if (device < 0) {
+    *out = p;
+    return FDLP_OK;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) MEL_FAIL(FDLP_E_HIP, "no HIP device visible");
+  if (device >= ndev) MEL_FAIL(FDLP_E_INVALID, "device index out of range");
+  if (hipSetDevice(device) != hipSuccess) MEL_FAIL(FDLP_E_HIP, "hipSetDevice failed");
+  MEL_TRY(upload(&p->d_win, win.data(), win.size()));
+  MEL_TRY(upload(&p->d_fb, fb.data(), fb.size()));
+  MEL_TRY(upload(&p->d_lo, lo.data(), lo.size()));
+  MEL_TRY(upload(&p->d_hi, hi.data(), hi.size()));
+  MEL_TRY(upload(&p->d_om, om.data(), om.size()));
+  MEL_TRY(upload(&p->d_rtw, rtw.data(), rtw.size()));
+  if (hipMalloc((void**)&p->d_frames, sizeof(fdlp::MelFrame) * c.max_frames) != hipSuccess ||
+      hipHostMalloc((void**)&p->h_frames, sizeof(fdlp::MelFrame) * c.max_frames, hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&p->staging_done, hipEventDisableTiming) != hipSuccess)
+    MEL_FAIL(FDLP_E_NOMEM, "mel plan workspace allocation failed");
+  fdlp::MelConsts& m = p->mc;
+  m.L = p->L; m.hop = p->hop; m.ext = p->ext; m.nfft = c.nfft; m.nh = nh; m.nbins = ncol;
+  m.nfilters = c.nfilters; m.power = c.power ? 1 : 0;
+  m.window = p->d_win; m.fbank = p->d_fb; m.lo = p->d_lo; m.hi = p->d_hi; m.om = p->d_om; m.rtw = p->d_rtw;
+  m.dp = dp;
+#undef MEL_FAIL
+#undef MEL_TRY
+  *out = p;
+  return FDLP_OK;
+}
+
+int fdlp_mel_plan_destroy(fdlp_mel_plan* p) { return free_mel_plan(p); }
+
+int fdlp_mel_geometry(const fdlp_mel_plan* p, int64_t T, int32_t* F) {
+  if (!p || !F || T < 0) return fail(FDLP_E_INVALID, "fdlp_mel_geometry: bad args");
+  *F = (int32_t)mel_frames_of(p, T);
+  return FDLP_OK;
+}
+
+int fdlp_mel_compute(fdlp_mel_plan* p, const fdlp_batch* b, void* stream) {
+  if (!p || !b || p->device < 0) return fail(FDLP_E_INVALID, "fdlp_mel_compute: bad args or host-only plan");
+  if (b->n_utt < 0 || (b->n_utt > 0 && (!b->pcm_dev || !b->pcm_off || !b->utt_len || !b->out_row)) ||
+      (!b->out_dev && !b->out_f64_dev))
+    return fail(FDLP_E_INVALID, "fdlp_mel_compute: bad batch");
+  if (b->noise_dev && (!b->noise_off || !b->noise_alpha)) return fail(FDLP_E_INVALID, "noise arrays missing");
+  if (b->preprocess == FDLP_PRE_DIFF && (b->pcm_kind != FDLP_PCM_I16 || b->noise_dev))
+    return fail(FDLP_E_INVALID, "diff preprocessing needs int16 PCM and no noise");
+  hipStream_t s = (hipStream_t)stream;
+  if (p->staging_pending) {
+    HIP_TRY(hipEventSynchronize(p->staging_done));
+    p->staging_pending = false;
+  }
+  int nf = 0;
+  for (int u = 0; u < b->n_utt; ++u) {
+    const int64_t T = b->utt_len[u];
+    if (T < 1) return fail(FDLP_E_INVALID, "empty utterance");
+    const int64_t F = mel_frames_of(p, T);
+    if (nf + F > p->cfg.max_frames) return fail(FDLP_E_CAPACITY, "batch exceeds the mel plan's max_frames");
+    for (int64_t k = 0; k < F; ++k) {
+      fdlp::MelFrame& fd = p->h_frames[nf++];
+      fd.pcm_off = b->pcm_off[u];
+      fd.noise_off = b->noise_dev ? b->noise_off[u] : -1;
+      fd.alpha = b->noise_dev ? b->noise_alpha[u] : 0.0;
+      fd.out_row = b->out_row[u] + k;
+      fd.T = (int32_t)T;
+      fd.k = (int32_t)k;
+    }
+  }
+  if (nf == 0) return FDLP_OK;
+  HIP_TRY(hipMemcpyAsync(p->d_frames, p->h_frames, sizeof(fdlp::MelFrame) * nf, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipEventRecord(p->staging_done, s));
+  p->staging_pending = true;
+  const int kind = b->preprocess == FDLP_PRE_DIFF ? 2 : b->pcm_kind;
+  HIP_TRY(fdlp::launch_mel(p->mc, p->d_frames, nf, b->pcm_dev, kind, b->noise_dev, b->out_dev, b->out_f64_dev,
+                           b->ark_decimals, s));
+  return FDLP_OK;
+}
+
 int fdlp_reverb(const fdlp_reverb_batch* b, void* stream) {
   if (!b || b->n_utt < 0 || !b->pcm_off || !b->utt_len || !b->rir_dev || b->rir_len < 1 || !b->out_dev ||
       !b->out_len || (b->n_utt > 0 && !b->pcm_dev) || (b->noise_dev && (!b->noise_off || !b->noise_alpha)) ||

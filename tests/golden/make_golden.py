@@ -188,6 +188,69 @@ def cli_options_fixture():
     print("wrote cli_options.json", len(opts))
 
 
+def run_reference_mel(signals, opts, noise_seed=None, noise=None, noise_name=None, rir=None):
+    """computeMelSpectrum.compute_mel_spectrum with get_kaldi_ark captured (copy-feats is absent)."""
+    sys.path.insert(0, os.path.join(REF, "src/featgen"))
+    import computeMelSpectrum as cm  # noqa: E402
+    captured = {}
+    cm.get_kaldi_ark = lambda feat_dict, outfile, kaldi_cmd='copy-feats': captured.update(
+        {k: np.array(v) for k, v in feat_dict.items()})
+    with tempfile.TemporaryDirectory() as td:
+        scp = os.path.join(td, "wav.scp")
+        with open(scp, "w") as f:
+            for utt, x in signals.items():
+                p = os.path.join(td, utt + ".wav")
+                wavfile.write(p, 16000, x)
+                f.write("%s %s\n" % (utt, p))
+        if noise is not None:
+            os.makedirs(os.path.join(td, "noises"), exist_ok=True)
+            wavfile.write(os.path.join(td, "noises", noise_name + ".wav"), 16000, noise)
+        if rir is not None:
+            os.makedirs(os.path.join(td, "RIR"), exist_ok=True)
+            wavfile.write(os.path.join(td, "RIR", "RIR_SmallRoom1_near_AnglA.wav"), 16000, rir)
+        cwd = os.getcwd()
+        os.chdir(td)
+        try:
+            ns = argparse.Namespace(scp=scp, outfile=os.path.join(td, "out"), scp_type="wav",
+                                    spectrum_type=opts.get("spectrum_type", "log"), nfilters=opts["nfilters"],
+                                    fduration=opts["fduration"], frate=opts["frate"], nfft=opts["nfft"],
+                                    add_reverb=opts.get("add_reverb", "clean"), fbank_type=opts["fbank_type"],
+                                    write_utt2num_frames=False, add_noise=opts.get("add_noise", "clean"))
+            if noise_seed is not None:
+                np.random.seed(noise_seed)
+            cm.compute_mel_spectrum(ns)
+        finally:
+            os.chdir(cwd)
+    return captured
+
+
+MEL_DEFAULT = dict(nfilters=23, fduration=0.02, frate=100, nfft=1024, fbank_type="mel,1", spectrum_type="log")
+
+
+def mel_fixtures():
+    """computeMelSpectrum.py (run_melspec baseline): default log-mel, recipe nfilters=15, power spectrum with
+    a cochlear filterbank, diff, and noise + reverb."""
+    sig = OrderedDict()
+    sig["m1"] = speech_like(16000, 81)
+    sig["m2"] = speech_like(23457, 82)
+    sig["mwhite"] = white(8000, 83)
+    sig["mshort"] = speech_like(700, 84)
+    save("mel_default", sig, MEL_DEFAULT, 0, run_reference_mel(sig, MEL_DEFAULT))
+    opts = dict(MEL_DEFAULT, nfilters=15)
+    save("mel_recipe15", sig, opts, 0, run_reference_mel(sig, opts))
+    opts = dict(MEL_DEFAULT, nfilters=40, nfft=512, fduration=0.025, fbank_type="cochlear,1,1,1,2.5,1",
+                spectrum_type="power")
+    save("mel_cochlear_power", sig, opts, 0, run_reference_mel(sig, opts))
+    opts = dict(MEL_DEFAULT, add_noise="diff")
+    save("mel_diff", sig, opts, 0, run_reference_mel(sig, opts))
+    rir = synthetic_rir(1200, 85)
+    noise = white(16000 * 3, 86, scale=1000.0)
+    opts = dict(MEL_DEFAULT, add_noise="babble,10", add_reverb="small_room")
+    save("mel_noise_reverb", sig, opts, 0,
+         run_reference_mel(sig, opts, noise_seed=7, noise=noise, noise_name="babble", rir=rir),
+         extra=dict(noise_seed=7), more={"rir": rir, "noise_babble": noise})
+
+
 def reverb_rir_fixture():
     """--add_reverb small_room (features.py:110-115) with a synthetic stereo RIR, clean and with noise."""
     rir = synthetic_rir(4000, 5)
@@ -209,6 +272,9 @@ def main():
     sys.dont_write_bytecode = True
     if "--reverb-only" in sys.argv:
         reverb_rir_fixture()
+        return
+    if "--mel-only" in sys.argv:
+        mel_fixtures()
         return
     cli_options_fixture()
     if "--cli-only" in sys.argv:
@@ -274,6 +340,7 @@ def main():
     save("gamma_lifter_odd", gw, opts, 13, feats, extra=dict(lifter=lif.tolist()))
     os.unlink(lifpath)
     reverb_rir_fixture()
+    mel_fixtures()
 
 
 if __name__ == "__main__":
