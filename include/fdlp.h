@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define FDLP_ABI_VERSION 1
+#define FDLP_ABI_VERSION 2
 
 enum {
   FDLP_OK = 0,
@@ -62,7 +62,17 @@ typedef struct fdlp_config {
   double support_eps;        /* filter taps < eps*peak are skipped in the autocorrelation
                                 (0 = every non-zero tap; DESIGN.md "support")            */
   int32_t max_frames;        /* workspace capacity: analysis frames per fdlp_compute call  */
+  /* ---- sibling feature: FDLP modulation spectrum (src/featgen/computeModulationSpectrum.py) ---- */
+  int32_t mode;              /* FDLP_MODE_SPECTROGRAM | FDLP_MODE_MODSPEC                          */
+  int32_t window;            /* analysis window: FDLP_WIN_HAMMING (spectrogram, :29) |
+                                FDLP_WIN_HANNING (modspec default, :30) | FDLP_WIN_RECT (--no_window) */
+  int32_t coeff_0;           /* modspec --coeff_0 (1-based first kept coefficient); --coeff_n = coeff_num */
+  int32_t keep_even;         /* modspec --keep_even (:66-72, :191-195)                              */
+  int32_t compensate_noise;  /* modspec --compensate_noise: x linspace(0, n/(2 fduration), coeff_n) (:82-88) */
+  int32_t absolute_value;    /* modspec --absolute_value (:186-187)                                 */
 } fdlp_config;
+enum { FDLP_MODE_SPECTROGRAM = 0, FDLP_MODE_MODSPEC = 1 };
+enum { FDLP_WIN_HAMMING = 0, FDLP_WIN_HANNING = 1, FDLP_WIN_RECT = 2 };
 
 typedef struct fdlp_plan fdlp_plan;
 
@@ -100,8 +110,11 @@ const char* fdlp_last_error(void);
 int fdlp_abi_version(void);
 
 /* Frame geometry of one utterance of T samples: F analysis frames (getFrames,
- * features.py:151) and L output frames (int(ceil(T*frate/srate)), :182). */
+ * features.py:151) and L output frames (int(ceil(T*frate/srate)), :182; L = F for the modspec
+ * mode, one feature row per analysis frame, computeModulationSpectrum.py:161). */
 int fdlp_geometry(const fdlp_plan* plan, int64_t T, int32_t* F, int32_t* L);
+/* Output feature dimension per row: nfilters (spectrogram) or nfilters * feat_len (modspec). */
+int fdlp_plan_out_dim(const fdlp_plan* plan, int32_t* dim);
 /* Plan constants: N (DCT length), nfft, hop, nlags (=order+2), kk (envelope length). */
 int fdlp_plan_info(const fdlp_plan* plan, int32_t* N, int32_t* hop, int32_t* nlags, int32_t* kk,
                    int32_t* ola_hop);

@@ -28,6 +28,11 @@ FDLP_PCM_F64 = 1
 FDLP_PRE_NONE = 0
 FDLP_PRE_DIFF = 1
 FDLP_NUM_STAGES = 5
+FDLP_MODE_SPECTROGRAM = 0
+FDLP_MODE_MODSPEC = 1
+FDLP_WIN_HAMMING = 0
+FDLP_WIN_HANNING = 1
+FDLP_WIN_RECT = 2
 STAGE_NAMES = ("frames_dft1", "dft2_dct", "autocorr", "lpc_env", "ola_log")
 
 c_i32, c_i64, c_dbl, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
@@ -48,6 +53,8 @@ class FdlpConfigC(ctypes.Structure):
         ("odd_mod_zero", c_i32), ("gamma_enabled", c_i32),
         ("gamma_scale", c_dbl), ("gamma_shape", c_dbl), ("gamma_pk", c_dbl),
         ("lifter", P_dbl), ("lifter_len", c_i32), ("support_eps", c_dbl), ("max_frames", c_i32),
+        ("mode", c_i32), ("window", c_i32), ("coeff_0", c_i32), ("keep_even", c_i32),
+        ("compensate_noise", c_i32), ("absolute_value", c_i32),
     ]
 
 
@@ -84,6 +91,7 @@ SIGNATURES = {
     "fdlp_abi_version": (c_i32, []),
     "fdlp_geometry": (c_i32, [c_p, c_i64, P_i32, P_i32]),
     "fdlp_plan_info": (c_i32, [c_p, P_i32, P_i32, P_i32, P_i32, P_i32]),
+    "fdlp_plan_out_dim": (c_i32, [c_p, P_i32]),
     "fdlp_plan_fbank": (c_i32, [c_p, P_dbl, P_i32, P_i32]),
     "fdlp_plan_weights": (c_i32, [c_p, P_dbl]),
     "fdlp_make_fbank": (c_i32, [ctypes.POINTER(FdlpConfigC), c_i32, P_dbl, P_i32]),
@@ -140,7 +148,7 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.fdlp_abi_version() != 1:
+    if lib.fdlp_abi_version() != 2:
         raise ImportError("libfdlp_hip.so ABI mismatch")
     return lib
 

@@ -133,6 +133,9 @@ struct RevUtt {
 hipError_t launch_reverb(const RevUtt* U, int n_utt, int64_t maxT, const void* pcm, int kind, int pre,
                          const int16_t* noise, const double* rir, int R, double* x, double* y, double* xs,
                          double* out, int64_t* out_len, hipStream_t s);
+hipError_t launch_modspec_out(const double* cep, const FrameDesc* frames, const UttDesc* utts, int nframes, int B,
+                              int M, int c0, int feat_len, int step, int first, const double* faxis, int absval,
+                              float* out, double* out64, int decimals, hipStream_t s);
 int cmvn_chunks(int64_t rows);
 hipError_t launch_cmvn(const float* x, int64_t rows, int D, double* part, double* stats, hipStream_t s);
 }  // namespace fdlp

@@ -2183,4 +2183,44 @@ hipError_t launch_mel(const MelConsts& c, const MelFrame* frames, int nframes, c
   return hipGetLastError();
 }
 
+// -----------------------------------------------------------------------------------------
+// 11. FDLP modulation spectrum output (src/featgen/computeModulationSpectrum.py:165-201): per frame and
+//     band, np.real(computeModSpecFromLpc(gg, a, coeff_n)) [* faxis] [abs] sliced [coeff_0-1 : coeff_n]
+//     (every other one with --keep_even), rows [frame, band * feat_len + i].  Thread per output value.
+// -----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void modspec_out_kernel(const double* __restrict__ cep,
+                                                          const FrameDesc* __restrict__ frames,
+                                                          const UttDesc* __restrict__ utts, int nframes, int B, int M,
+                                                          int c0, int feat_len, int step, int first,
+                                                          const double* __restrict__ faxis, int absval,
+                                                          float* __restrict__ out, double* __restrict__ out64,
+                                                          int decimals, double scale10) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t per = (int64_t)B * feat_len;
+  if (e >= (int64_t)nframes * per) return;
+  const int f = (int)(e / per);
+  const int r = (int)(e % per);
+  const int j = r / feat_len, i = r % feat_len;
+  const int n = c0 + first + step * i;
+  double v = cep[((int64_t)f * B + j) * M + n];
+  if (faxis) v = v * faxis[n];
+  if (absval) v = fabs(v);
+  const FrameDesc fd = frames[f];
+  const int64_t o = (utts[fd.utt].out_row + fd.k) * per + r;
+  if (out64) out64[o] = v;
+  if (out) out[o] = decimals >= 0 ? (float)(nearbyint(v * scale10) / scale10) : (float)v;
+}
+
+hipError_t launch_modspec_out(const double* cep, const FrameDesc* frames, const UttDesc* utts, int nframes, int B,
+                              int M, int c0, int feat_len, int step, int first, const double* faxis, int absval,
+                              float* out, double* out64, int decimals, hipStream_t s) {
+  const int64_t total = (int64_t)nframes * B * feat_len;
+  if (total <= 0) return hipSuccess;
+  double scale10 = 1.0;
+  for (int i = 0; i < decimals; ++i) scale10 *= 10.0;
+  hipLaunchKernelGGL(modspec_out_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, cep, frames, utts,
+                     nframes, B, M, c0, feat_len, step, first, faxis, absval, out, out64, decimals, scale10);
+  return hipGetLastError();
+}
+
 }  // namespace fdlp

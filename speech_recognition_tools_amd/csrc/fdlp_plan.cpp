@@ -258,6 +258,10 @@ struct fdlp_plan {
   double *d_sk_e = nullptr, *r_up = nullptr;
   fdlp::SkSnap* d_sk_snap = nullptr;
   int2* d_sk_reg = nullptr;
+  // modulation-spectrum mode (computeModulationSpectrum.py)
+  bool modspec = false;
+  int feat_len = 0, out_dim = 0;
+  double* d_faxis = nullptr;  // [coeff_n] compensate_noise multipliers, null otherwise
   std::vector<std::vector<hipEvent_t>> prof_pending;
   double prof_ms[FDLP_NUM_STAGES] = {0};
   int prof_calls = 0;
@@ -293,7 +297,7 @@ int free_plan(fdlp_plan* p) {
   void* devs[] = {p->d_fbank, p->d_hamming, p->d_weights, p->d_env_cos, p->d_env_win, p->d_tw1, p->d_post, p->d_rtw,
                   p->d_om1, p->d_om2, p->d_lo, p->d_hi, p->ws.z, p->ws.dct, p->ws.r, p->ws.a, p->ws.gg,
                   p->ws.cep, p->ws.env, p->d_frames, p->d_utts, p->d_sk_e, p->r_up, p->d_sk_snap,
-                  p->d_sk_reg};
+                  p->d_sk_reg, p->d_faxis};
   for (void* d : devs)
     if (d) (void)hipFree(d);
   if (p->h_frames) (void)hipHostFree(p->h_frames);
@@ -321,6 +325,7 @@ int64_t frames_of(const fdlp_plan* p, int64_t T) {
 }
 
 int64_t out_of(const fdlp_plan* p, int64_t T) {
+  if (p->modspec) return frames_of(p, T);  // one row per analysis frame (computeModulationSpectrum.py:161)
   // int(np.ceil(T*frate/srate))  (computeFDLPSpectrogram.py:182)
   return (int64_t)ceil((double)(T * (int64_t)p->cfg.frate) / (double)p->cfg.srate);
 }
@@ -387,6 +392,9 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   p->N = (int)((double)c.srate * c.fduration);                       // features.py:134
   const double lfr = 1.0 / (ov * c.fduration);                       // :174
   p->hop = (int)((double)c.srate / lfr);                             // features.py:135
+  p->modspec = c.mode == FDLP_MODE_MODSPEC;
+  if (c.mode != FDLP_MODE_SPECTROGRAM && !p->modspec) PLAN_FAIL(FDLP_E_INVALID, "unknown plan mode");
+  if (p->modspec) p->hop = (int)((double)c.srate / (double)c.frate);  // getFrames(.., frate, ..) (:150-151)
   if (p->N % 2 == 0) { p->sp_b = p->N / 2 - 1; p->sp_f = p->N / 2; p->ext = p->N / 2 - 1; }
   else { p->sp_b = p->sp_f = p->ext = (p->N - 1) / 2; }
   p->nfft = (int)(2.0 * c.fduration * (double)c.srate);              // :53, :59
@@ -398,10 +406,19 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   p->p = c.order;
   p->M = c.coeff_num;
   p->nlags = c.order + 2;
+  if (p->modspec) {  // no envelope / OLA: a minimal envelope for the shared LPC kernel, output = cepstra
+    p->env_nfft = 2; p->kk = 1; p->kkb2 = 0; p->ola_hop = 1;
+    if (c.coeff_0 < 1 || c.coeff_0 > c.coeff_num) PLAN_FAIL(FDLP_E_INVALID, "modspec needs 1 <= coeff_0 <= coeff_n");
+    if (c.gamma_enabled || c.lifter || c.odd_mod_zero) PLAN_FAIL(FDLP_E_INVALID, "modspec takes no gamma/lifter/odd options");
+    const int sel = c.coeff_num - c.coeff_0 + 1;                     // coeff_num (:64)
+    p->feat_len = c.keep_even ? ((c.coeff_0 % 2 == 0) ? sel / 2 : (sel + 1) / 2) : sel;  // :66-80
+    if (p->feat_len < 1) PLAN_FAIL(FDLP_E_INVALID, "modspec selects no coefficient");
+  }
   p->Me = std::min(p->M, p->env_nfft);
+  p->out_dim = p->modspec ? c.nfilters * p->feat_len : c.nfilters;
   if (p->N < 2 || p->hop < 1) PLAN_FAIL(FDLP_E_INVALID, "frame length / hop too small");
   if (p->kk < 1 || p->env_nfft < 1 || p->kk > p->env_nfft) PLAN_FAIL(FDLP_E_INVALID, "fduration*frate too small");
-  if (p->ola_hop < p->kkb2) PLAN_FAIL(FDLP_E_INVALID, "unsupported: negative OLA pointer (overlap too large)");
+  if (!p->modspec && p->ola_hop < p->kkb2) PLAN_FAIL(FDLP_E_INVALID, "unsupported: negative OLA pointer (overlap too large)");
   if (fdlp::autocorr_tiles(p->nlags) > 16) PLAN_FAIL(FDLP_E_INVALID, "order too large (max 238)");
   if (p->N < 1024) PLAN_FAIL(FDLP_E_INVALID, "frame length int(srate*fduration) must be >= 1024 samples");
   if ((p->p + 1 + 15) / 16 > 15) PLAN_FAIL(FDLP_E_INVALID, "order too large for the Levinson kernel");
@@ -448,7 +465,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   // modulation weights (:94-118)
   const int M = p->M;
   p->weights_host.assign((size_t)3 * M, 1.0);
-  for (int i = 0; i < M; ++i) p->weights_host[i] = (i >= c.coeff_lp && i <= c.coeff_hp) ? 1.0 : 0.0;
+  for (int i = 0; i < M; ++i) p->weights_host[i] = (p->modspec || (i >= c.coeff_lp && i <= c.coeff_hp)) ? 1.0 : 0.0;
   if (cfg->lifter) {
     if (cfg->lifter_len != M) PLAN_FAIL(FDLP_E_INVALID, "lifter_config must hold coeff_num values (reference broadcast)");
     for (int i = 0; i < M; ++i) p->weights_host[M + i] = cfg->lifter[i];
@@ -464,7 +481,12 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   }
 
   // windows and tables
-  const std::vector<double> ham = cos_window(p->N, 0.54, 0.46);
+  // analysis window: np.hamming (spectrogram, :29), np.hanning (modspec default :30), ones (--no_window)
+  std::vector<double> ham;
+  if (c.window == FDLP_WIN_HAMMING) ham = cos_window(p->N, 0.54, 0.46);
+  else if (c.window == FDLP_WIN_HANNING) ham = cos_window(p->N, 0.5, 0.5);
+  else if (c.window == FDLP_WIN_RECT) ham.assign(p->N, 1.0);
+  else PLAN_FAIL(FDLP_E_INVALID, "unknown analysis window");
   const std::vector<double> hann_k = cos_window(p->kk, 0.5, 0.5), hamm_k = cos_window(p->kk, 0.54, 0.46);
   std::vector<double> env_win(2 * (size_t)p->kk);
   for (int t = 0; t < p->kk; ++t) { env_win[2 * t] = hann_k[t]; env_win[2 * t + 1] = hamm_k[t]; }
@@ -516,6 +538,11 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   PLAN_TRY(upload(&p->d_lo, p->lo.data(), p->lo.size()));
   PLAN_TRY(upload(&p->d_hi, p->hi.data(), p->hi.size()));
   PLAN_TRY(upload(&p->d_hamming, ham.data(), ham.size()));
+  if (p->modspec && c.compensate_noise) {  // faxis = linspace(0, coeff_num / (2 fduration), coeff_n) (:86-88)
+    const double fmax = (double)(c.coeff_num - c.coeff_0 + 1) / (2.0 * c.fduration);
+    const std::vector<double> fax = linspace(0.0, fmax, c.coeff_num);
+    PLAN_TRY(upload(&p->d_faxis, fax.data(), fax.size()));
+  }
   PLAN_TRY(upload(&p->d_weights, p->weights_host.data(), p->weights_host.size()));
   PLAN_TRY(upload(&p->d_env_cos, env_cos.data(), env_cos.size()));
   PLAN_TRY(upload(&p->d_env_win, env_win.data(), env_win.size()));
@@ -574,6 +601,12 @@ int fdlp_geometry(const fdlp_plan* p, int64_t T, int32_t* F, int32_t* L) {
   if (!p || T < 0) return fail(FDLP_E_INVALID, "fdlp_geometry: bad args");
   if (F) *F = (int32_t)frames_of(p, T);
   if (L) *L = (int32_t)out_of(p, T);
+  return FDLP_OK;
+}
+
+int fdlp_plan_out_dim(const fdlp_plan* p, int32_t* dim) {
+  if (!p || !dim) return fail(FDLP_E_INVALID, "fdlp_plan_out_dim: bad args");
+  *dim = p->out_dim;
   return FDLP_OK;
 }
 
@@ -657,10 +690,12 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     if (L > INT32_MAX / 2) return fail(FDLP_E_INVALID, "utterance too long");
     if (nf + F > p->max_frames) return fail(FDLP_E_CAPACITY, "batch exceeds the plan's max_frames");
     if (b->noise_dev && b->noise_off[u] < 0) return fail(FDLP_E_INVALID, "negative noise offset");
-    dst.resize(F); src.resize(F); cnt.resize(F);
-    int rc = ola_table(p, (int)F, (int)L, jit, dst.data(), src.data(), cnt.data());
-    if (rc != FDLP_OK) return rc;
-    if (jit) jit += F - 1;
+    dst.assign(F, 0); src.assign(F, 0); cnt.assign(F, 0);
+    if (!p->modspec) {
+      int rc = ola_table(p, (int)F, (int)L, jit, dst.data(), src.data(), cnt.data());
+      if (rc != FDLP_OK) return rc;
+      if (jit) jit += F - 1;
+    }
     for (int64_t k = 0; k < F; ++k) {
       fdlp::FrameDesc& fd = p->h_frames[nf + k];
       fd.pcm_off = b->pcm_off[u];
@@ -710,7 +745,7 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     double* env = p->ws.env + it0 * p->kk;
     double* a_dbg = p->debug_intermediates ? p->ws.a + it0 * (p->p + 1) : nullptr;
     double* gg_dbg = p->debug_intermediates ? p->ws.gg + it0 : nullptr;
-    double* cep_dbg = p->debug_intermediates ? p->ws.cep + it0 * p->M : nullptr;
+    double* cep_dbg = (p->debug_intermediates || p->modspec) ? p->ws.cep + it0 * p->M : nullptr;
     HIP_TRY(mark(0));
     HIP_TRY(fdlp::launch_frames_dft1(p->dc, p->d1, p->d2.n, b->pcm_dev,
                                      b->preprocess == FDLP_PRE_DIFF ? 2 : b->pcm_kind, b->noise_dev, p->d_frames + f0,
@@ -720,7 +755,7 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     HIP_TRY(mark(2));
     if (p->ac_path == FDLP_AC_STRUCTURED) {
       HIP_TRY(fdlp::launch_autocorr_structured(p->dc, p->ws.dct + f0 * N, n, r, p->r_up + it0 * nl, st));
-    } else if (p->fused && !p->debug_intermediates) {
+    } else if (p->fused && !p->debug_intermediates && !p->modspec) {
       // autocorrelation + LPC tail in one launch (stage 3 is then empty)
       HIP_TRY(fdlp::launch_band_fused(p->dc, p->cfg.odd_mod_zero, p->ws.dct + f0 * N, its, r, env, st));
       HIP_TRY(mark(3));
@@ -749,8 +784,16 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     HIP_TRY(hipStreamWaitEvent(s, p->ev_join, 0));
   }
   if (p->profiling) HIP_TRY(hipEventRecord(ev[ev.size() - 2], s));
-  HIP_TRY(fdlp::launch_ola_log(p->dc, p->ws.env, p->d_frames, p->d_utts, b->n_utt, maxL, b->out_dev,
-                               b->out_f64_dev, b->ark_decimals, s));
+  if (p->modspec) {  // mod_spec[coeff_0-1 : coeff_n] per band (computeModulationSpectrum.py:182-201)
+    const fdlp_config& c = p->cfg;
+    const int keep_odd_slot = c.keep_even && c.coeff_0 % 2 == 0 ? 1 : 0;  // temp2[1::2] vs temp2[0::2]
+    HIP_TRY(fdlp::launch_modspec_out(p->ws.cep, p->d_frames, p->d_utts, (int)nf, p->B, p->M, c.coeff_0 - 1,
+                                     p->feat_len, c.keep_even ? 2 : 1, keep_odd_slot, p->d_faxis,
+                                     c.absolute_value, b->out_dev, b->out_f64_dev, b->ark_decimals, s));
+  } else {
+    HIP_TRY(fdlp::launch_ola_log(p->dc, p->ws.env, p->d_frames, p->d_utts, b->n_utt, maxL, b->out_dev,
+                                 b->out_f64_dev, b->ark_decimals, s));
+  }
   if (p->profiling) {
     HIP_TRY(hipEventRecord(ev.back(), s));
     p->prof_pending.push_back(ev);

@@ -33,6 +33,13 @@ class FeatureConfig:
     lifter: Optional[Sequence[float]] = None
     srate: int = 16000
     support_eps: float = DEFAULT_SUPPORT_EPS
+    # modulation spectrum (computeModulationSpectrum.py): mode "modspec", coeff_num = --coeff_n
+    mode: str = "spectrogram"
+    window: str = "hamming"           # "hamming" (:29) | "hanning" (modspec :30) | "rect" (--no_window)
+    coeff_0: int = 1
+    keep_even: bool = False
+    compensate_noise: bool = False
+    absolute_value: bool = False
 
     def to_c(self, max_frames: int):
         c = FdlpConfigC()
@@ -65,6 +72,11 @@ class FeatureConfig:
             c.lifter, c.lifter_len = ptr(keep, ctypes.c_double), keep.size
         c.support_eps = float(self.support_eps)
         c.max_frames = int(max_frames)
+        c.mode = {"spectrogram": _lib.FDLP_MODE_SPECTROGRAM, "modspec": _lib.FDLP_MODE_MODSPEC}[self.mode]
+        c.window = {"hamming": _lib.FDLP_WIN_HAMMING, "hanning": _lib.FDLP_WIN_HANNING,
+                    "rect": _lib.FDLP_WIN_RECT}[self.window]
+        c.coeff_0, c.keep_even = int(self.coeff_0), int(bool(self.keep_even))
+        c.compensate_noise, c.absolute_value = int(bool(self.compensate_noise)), int(bool(self.absolute_value))
         return c, keep
 
     @staticmethod
@@ -119,6 +131,9 @@ class FdlpPlan:
         check(lib.fdlp_plan_info(h, *[ctypes.byref(x) for x in v]))
         self.N, self.hop, self.nlags, self.kk, self.ola_hop = (x.value for x in v)
         self.B = int(cfg.nfilters)
+        d = _lib.c_i32()
+        check(lib.fdlp_plan_out_dim(h, ctypes.byref(d)))
+        self.out_dim = d.value  # nfilters, or nfilters * feat_len in the modspec mode
 
     def close(self):
         h = getattr(self, "_h", None)
@@ -192,12 +207,13 @@ class FdlpPlan:
         rows[1:] = np.cumsum(Ls)
         total = int(rows[-1])
         dev = pcm.device
+        D = self.out_dim
         if out is None:
-            out = torch.empty((total, self.B), dtype=torch.float32, device=dev)
-        elif out.shape[0] < total or out.shape[1] != self.B or out.dtype != torch.float32:
+            out = torch.empty((total, D), dtype=torch.float32, device=dev)
+        elif out.shape[0] < total or out.shape[1] != D or out.dtype != torch.float32:
             raise ValueError("out buffer too small")
-        out64 = torch.empty((total, self.B), dtype=torch.float64, device=dev) if want_f64 else None
-        jit = np.ascontiguousarray(jitter, dtype=np.uint8)
+        out64 = torch.empty((total, D), dtype=torch.float64, device=dev) if want_f64 else None
+        jit = np.ascontiguousarray(np.zeros(1) if jitter is None else jitter, dtype=np.uint8)
         b = FdlpBatchC()
         b.n_utt, b.pcm_kind, b.pcm_dev = n, kind, pcm.data_ptr()
         b.pcm_off, b.utt_len, b.jitter = ptr(offs, ctypes.c_int64), ptr(lens, ctypes.c_int64), ptr(jit, ctypes.c_uint8)

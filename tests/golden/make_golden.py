@@ -251,6 +251,48 @@ def mel_fixtures():
          extra=dict(noise_seed=7), more={"rir": rir, "noise_babble": noise})
 
 
+def run_reference_modspec(signals, opts):
+    """computeModulationSpectrum.getFeats with dict2Ark captured (copy-feats is absent)."""
+    sys.path.insert(0, os.path.join(REF, "src/featgen"))
+    import computeModulationSpectrum as cms  # noqa: E402
+    captured = {}
+    cms.dict2Ark = lambda feat_dict, outfile, kaldi_cmd: captured.update({k: np.array(v) for k, v in feat_dict.items()})
+    with tempfile.TemporaryDirectory() as td:
+        scp = os.path.join(td, "wav.scp")
+        with open(scp, "w") as f:
+            for utt, x in signals.items():
+                p = os.path.join(td, utt + ".wav")
+                wavfile.write(p, 16000, x)
+                f.write("%s %s\n" % (utt, p))
+        ns = argparse.Namespace(scp=scp, outfile=os.path.join(td, "out"), scp_type="wav", add_reverb="clean",
+                                coeff_0=opts["coeff_0"], coeff_n=opts["coeff_n"], order=opts["order"],
+                                fduration=opts["fduration"], frate=opts["frate"], nfilters=opts["nfilters"],
+                                kaldi_cmd="true", fbank_type=opts["fbank_type"], complex_modulation=False,
+                                keep_even=opts.get("keep_even", False),
+                                compensate_noise=opts.get("compensate_noise", False),
+                                no_window=opts.get("no_window", False),
+                                absolute_value=opts.get("absolute_value", False), set_unity_gain=False)
+        cms.getFeats(ns)
+    return captured
+
+
+MODSPEC_DEFAULT = dict(nfilters=15, coeff_0=5, coeff_n=30, order=50, fduration=0.5, frate=100, fbank_type="mel,1")
+
+
+def modspec_fixtures():
+    """computeModulationSpectrum.py (make_modspec_feats.sh defaults) and its option variants."""
+    sig = OrderedDict()
+    sig["q1"] = speech_like(9000, 91)
+    sig["q2"] = speech_like(4100, 92)
+    sig["qwhite"] = white(3000, 93)
+    save("modspec_default", sig, MODSPEC_DEFAULT, 0, run_reference_modspec(sig, MODSPEC_DEFAULT))
+    opts = dict(MODSPEC_DEFAULT, keep_even=True, compensate_noise=True, absolute_value=True)
+    save("modspec_even_comp_abs", sig, opts, 0, run_reference_modspec(sig, opts))
+    opts = dict(MODSPEC_DEFAULT, nfilters=20, coeff_0=2, coeff_n=24, order=40, fduration=0.4, frate=50,
+                fbank_type="cochlear,1,1,1,2.5,1", keep_even=True, no_window=True)
+    save("modspec_cochlear_rect", sig, opts, 0, run_reference_modspec(sig, opts))
+
+
 def reverb_rir_fixture():
     """--add_reverb small_room (features.py:110-115) with a synthetic stereo RIR, clean and with noise."""
     rir = synthetic_rir(4000, 5)
@@ -275,6 +317,9 @@ def main():
         return
     if "--mel-only" in sys.argv:
         mel_fixtures()
+        return
+    if "--modspec-only" in sys.argv:
+        modspec_fixtures()
         return
     cli_options_fixture()
     if "--cli-only" in sys.argv:
@@ -341,6 +386,7 @@ def main():
     os.unlink(lifpath)
     reverb_rir_fixture()
     mel_fixtures()
+    modspec_fixtures()
 
 
 if __name__ == "__main__":
