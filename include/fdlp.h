@@ -143,12 +143,16 @@ int fdlp_set_debug(fdlp_plan* plan, int32_t keep_intermediates);
 /* Autocorrelation algorithm (stage 2).  FDLP_AC_DIRECT: per band, over the taps >= support_eps *
  * peak.  FDLP_AC_STRUCTURED: exact (no tap truncation) skirt-factorised algorithm for the cochlear
  * filterbank with a fixed slope (fbank_type cochlear,..,fixed=1,..; DESIGN.md "Structured
- * autocorrelation").  FDLP_AC_AUTO (plan default) picks STRUCTURED when the filterbank allows it.
- * fdlp_set_autocorr_path returns FDLP_E_INVALID when STRUCTURED is not available;
- * fdlp_autocorr_path returns the path in use (DIRECT or STRUCTURED) or a negative error code. */
+ * autocorrelation"), its three sweeps (lower skirt, flat tops, upper skirt) lag-parallel on the fp64
+ * VALU; FDLP_AC_STRUCTURED_MFMA: the same algorithm with MFMA lag-tile skirt sweeps and per-band
+ * flat tops (also used when the VALU sweeps do not fit: more than 256 lags or 8 overlapping flat
+ * tops).  FDLP_AC_AUTO (plan default) picks the first available of STRUCTURED, STRUCTURED_MFMA,
+ * DIRECT.  fdlp_set_autocorr_path returns FDLP_E_INVALID when the structured paths are not
+ * available; fdlp_autocorr_path returns the path in use or a negative error code. */
 #define FDLP_AC_AUTO 0
 #define FDLP_AC_DIRECT 1
 #define FDLP_AC_STRUCTURED 2
+#define FDLP_AC_STRUCTURED_MFMA 3
 int fdlp_set_autocorr_path(fdlp_plan* plan, int32_t path);
 int fdlp_autocorr_path(const fdlp_plan* plan);
 /* Lower-skirt / flat-top / upper-skirt split of every band, [0,m1) [m1,m2) [m2,N), used by the

@@ -43,6 +43,12 @@ struct SkSnap {
   double K;
 };
 
+// One event of the flat-top sweep (ac_vsweep_kernel): at sweep position S (after the positions >= S
+// are consumed) restart (type 0) or emit (type 1) chain `chain`, which serves band `band`.
+struct FlatEv {
+  int32_t S, band, type, chain;
+};
+
 // Device-resident constants of a plan.
 struct DevConsts {
   int B, N, hop, ext, p, nlags, M, Me, kk, env_nfft;
@@ -63,6 +69,10 @@ struct DevConsts {
                            // K_j = 10^(a (w - 2 fc_j + 2 c0)) / K'_j = 10^(b (2 fc_j + w - 2 c0))
   const int2* sk_reg;      // [B] (m1_j, m2_j): lower skirt [0,m1), flat top [m1,m2), upper skirt [m2,N)
   int sk_min[2];           // smallest threshold per skirt
+  // lag-parallel VALU sweeps (ac_vsweep_kernel); fl_ev null when not used
+  const FlatEv* fl_ev = nullptr;  // [fl_nev] flat-top events sorted by S descending
+  int fl_nev = 0, fl_C = 0;       // event count, chains needed (bands j and j - C never overlap)
+  int fl_lo = 0, fl_hi = 0;       // min m1, max m2
 };
 
 }  // namespace fdlp
@@ -88,7 +98,9 @@ hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const 
 hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* dense_rows,
                            int nframes_or_items, double* r, hipStream_t s);
 hipError_t launch_autocorr_structured(const DevConsts& c, const double* dct, int nframes, double* r,
-                                      double* rup, hipStream_t s);
+                                      double* rup, double* rflat, hipStream_t s);
+int vsweep_lanes_lags(int nlags);   // lags per lane of ac_vsweep_kernel, 0 = unsupported
+int vsweep_chains(int C);           // chain count instantiated for C needed chains, 0 = unsupported
 hipError_t launch_levinson(const DevConsts& c, const double* r, int items, double* a,
                            double* gg, hipStream_t s);
 hipError_t launch_cepstrum(int p, int M, const double* a, const double* gg, int items,

@@ -821,10 +821,12 @@ __global__ __launch_bounds__(64, 2) void ac_sweep_kernel(DevConsts c, const doub
 // circular wrap at N (true taps W_j D), plus the two skirt snapshots from ac_sweep_kernel:
 //   r_j[l] = K_j R_y(N-m1_j)[l] + flat + straddles + K'_j R_z(m2_j)[l]
 // r holds the lower-skirt term on entry and r_j on exit.
-template <int NT>
+// VS: the flat-top pairs come from ac_vsweep_kernel (rflat, right ends up to N), so the flat-top
+// loop is skipped and the m2 straddle takes B = (W - 1) D on [m2, N) (W D past the wrap).
+template <int NT, bool VS>
 __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const double* __restrict__ dct,
                                                         double* __restrict__ r, const double* __restrict__ rup,
-                                                        int items) {
+                                                        const double* __restrict__ rflat, int items) {
   static_assert(16 * NT <= kAcChunk, "window halo must fit one chunk");
   constexpr int kEpi = (32 + 31) * 17;                   // diag_blocks<NT, 32> image
   constexpr int kWin = (16 * NT + 63) / 64 * 64;         // A window of a straddle (>= nlags - 1)
@@ -849,7 +851,7 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
   for (int t = 0; t < NT; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
 
   // flat top: x = D on [m1, m2), 0 elsewhere
-  {
+  if constexpr (!VS) {
     const int lo = m1, hi = m2;
     const int nsteps = (hi - lo + 63) / 64;
     const int nchunks = (nsteps + kAcPer - 1) / kAcPer;
@@ -914,7 +916,11 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
       const int q = 64 * u + lane;
       const int pos = b - kWin + q;
       const double x = pos >= lb ? wv[u] * dv[u] : 0.0;
-      if (q < kWin + 16 * NT) xb[q] = pos >= b ? x : 0.0;
+      if constexpr (VS) {
+        if (q < kWin + 16 * NT) xb[q] = pos >= b ? (e == 1 && pos < N ? (wv[u] - 1.0) * dv[u] : x) : 0.0;
+      } else {
+        if (q < kWin + 16 * NT) xb[q] = pos >= b ? x : 0.0;
+      }
       if (q < kWin) xa[q] = pos < b ? x : 0.0;
     }
     __syncthreads();
@@ -931,7 +937,279 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
   __syncthreads();
   double* ro = r + (int64_t)item * nlags;
   const double* uo = rup + (int64_t)item * nlags;
-  diag_blocks<NT, 32>(acc, xs, nlags, lane, [&](int L, double v) { ro[L] = v + ro[L] + uo[L]; });
+  if constexpr (VS) {
+    const double* fo = rflat + (int64_t)item * nlags;
+    diag_blocks<NT, 32>(acc, xs, nlags, lane, [&](int L, double v) { ro[L] = v + ro[L] + uo[L] + fo[L]; });
+  } else {
+    diag_blocks<NT, 32>(acc, xs, nlags, lane, [&](int L, double v) { ro[L] = v + ro[L] + uo[L]; });
+  }
+}
+
+// -----------------------------------------------------------------------------------------
+// 3t. The three sweeps of the structured autocorrelation on the fp64 VALU, lag-parallel.
+//     Measured on MI355X: fp64 VALU FMA sustains ~75 TFLOP/s against ~51 for v_mfma_f64_16x16x4f64,
+//     and with every lane owning whole lags a snapshot is a plain register store (the MFMA lag
+//     tiles need a diagonal-sum epilogue per snapshot).
+//     Unit = one 16-lane DPP row = one (frame, sweep); 4 frames of the same sweep per wave, so the
+//     thresholds are wave-uniform.  Lane l owns lags A l .. A l + A - 1 (16 A >= nlags).  Sweep
+//     signal s[n] (n in sweep order, 0 past N):
+//       kind 0  lower skirt  s[n] = E[N-1-n] D[N-1-n]   snapshots K_j R(N - m1_j) -> rlow
+//       kind 1  upper skirt  s[n] = E'[n] D[n]          snapshots K'_j R(m2_j)    -> rup
+//       kind 2  flat tops    s[n] = D[n]                flat_j = sum_{m in [m1_j, m2_j)} D[m] D[m+l]
+//                                                       (right ends up to N)       -> rflat
+//     with R(S)[l] = sum_{n >= S} s[n] s[n+l].  Positions are consumed top-down in blocks of A:
+//       acc[u] += sum_{v<A} s[n0+v] * s[n0+v+A l+u]
+//     s[n0+v] comes from lane v of the row by DPP row_newbcast (one v_mov_b64_dpp per A FMAs), the
+//     window s[n0 + A l + q], q < 2A-1, from the current block's A loads and the previous block's
+//     (two register banks, so nothing is copied).  A threshold inside a block splits it into two
+//     masked passes.  Flat tops: no subtraction of suffix sums (that cancels when the spectrum above
+//     a band dominates it): the accumulator holds the positions since the last event and is added
+//     into C chains at each event; band j owns chain j mod C from its restart at m2_j to its
+//     emission at m1_j (C chosen on the host so that bands j and j - C never overlap).
+//     s is staged per unit in an LDS ring of 512 (+16 mirrored) positions, 128 at a time, the next
+//     128 prefetched into registers.
+// -----------------------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ double row_bcast(double v) {
+  // row_newbcast:K; every lane has a source, and bound_ctrl spares the 'old' operand (no init, no nops)
+  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + K, 0xF, 0xF, true);
+}
+
+constexpr int kVsRing = 512;
+constexpr int kVsMirror = 16;
+constexpr int kVsChunk = 64;
+
+template <int A, int V = 0>
+__device__ __forceinline__ void vs_bcast_all(double (&bb)[A], double cur) {
+  if constexpr (V < A) {
+    bb[V] = row_bcast<V>(cur);
+    vs_bcast_all<A, V + 1>(bb, cur);
+  }
+}
+// all A broadcasts first (their DPP latency is then hidden behind the FMAs of the earlier ones)
+template <int A>
+__device__ __forceinline__ void vs_fma_block(double (&acc)[A], double cur, const double (&lo)[A],
+                                             const double (&hi)[A]) {
+  double bb[A];
+  vs_bcast_all<A>(bb, cur);
+#pragma unroll
+  for (int v = 0; v < A; ++v)
+#pragma unroll
+    for (int u = 0; u < A; ++u) acc[u] = fma(bb[v], (v + u < A) ? lo[v + u] : hi[v + u - A], acc[u]);
+}
+
+template <int A, int C>
+__global__ __launch_bounds__(64, 2) void ac_vsweep_kernel(DevConsts c, const double* __restrict__ dct,
+                                                          double* __restrict__ rlow, double* __restrict__ rup,
+                                                          double* __restrict__ rflat,
+                                                          const SkSnap* __restrict__ snaps,
+                                                          const FlatEv* __restrict__ fev, int nframes,
+                                                          int ngroups) {
+  // snaps / fev (= c.sk_snap / c.fl_ev) as restrict parameters: not clobbered by the output stores,
+  // so their wave-uniform reads become scalar loads
+  static_assert(A % 2 == 0 && A <= 16 && 18 * A < kVsRing - kVsChunk && A <= kVsMirror + 1, "vsweep geometry");
+  __shared__ double ring_all[4][kVsRing + kVsMirror];
+  // C == 0: the two skirt sweeps, item = 2 group + skirt (a frame group's two sweeps adjacent on one
+  // XCD, so its D rows are read from HBM once); C > 0: the flat-top sweep, item = group
+  const int item = xcd_item();
+  if (item >= (C == 0 ? 2 : 1) * ngroups) return;
+  const int g = C == 0 ? item >> 1 : item;
+  const int kind = C == 0 ? (item & 1) : 2;
+  const int lane = threadIdx.x;
+  const int row = lane >> 4;
+  const int l = lane & 15;
+  const int f = 4 * g + row;
+  const bool fvalid = f < nframes;
+  const int N = c.N, B = c.B, nlags = c.nlags;
+  const double* drow = dct + (int64_t)(fvalid ? f : 0) * N;
+  const double* ew = c.sk_e + (int64_t)(kind == 1 ? N : 0);
+  double* rg = ring_all[row];
+  const int nlo = kind == 2 ? c.fl_lo : c.sk_min[kind];
+  const int nhi = kind == 2 ? c.fl_hi : N;
+  if (nhi <= nlo) {  // nothing to sweep: every snapshot / emission is zero
+    const int nev = kind == 2 ? c.fl_nev : B;
+    for (int k = 0; k < nev; ++k) {
+      const int band = kind == 2 ? fev[k].band : snaps[kind * B + k].band;
+      if (kind == 2 && fev[k].type == 0) continue;
+      double* o = (kind == 0 ? rlow : (kind == 1 ? rup : rflat)) + ((int64_t)f * B + band) * nlags;
+#pragma unroll
+      for (int u = 0; u < A; ++u)
+        if (fvalid && A * l + u < nlags) o[A * l + u] = 0.0;
+    }
+    return;
+  }
+
+  // ---- staging: value at sweep position n, prefetched 128 positions ahead ----------------------
+  constexpr int kPf = kVsChunk / 16;
+  double pf[kPf], pe[C == 0 ? kPf : 1];
+  // unconditional (clamped) loads: no branches around them, and their registers are read only in
+  // commit, one chunk later, so the wait for them is not pulled into the FMA loop
+  auto issue = [&](int base) {
+#pragma unroll
+    for (int q = 0; q < kPf; ++q) {
+      const int n = min(max(base + 16 * q + l, 0), N - 1);
+      const int m = kind == 0 ? N - 1 - n : n;
+      pf[q] = __builtin_nontemporal_load(drow + m);
+      if constexpr (C == 0) pe[q] = ew[m];
+    }
+  };
+  auto commit = [&](int base) {
+#pragma unroll
+    for (int q = 0; q < kPf; ++q) {
+      const int n = base + 16 * q + l;
+      const int slot = n & (kVsRing - 1);
+      double v = pf[q];
+      if constexpr (C == 0) v = pe[q] * v;
+      v = (n >= 0 && n < N) ? v : 0.0;
+      rg[slot] = v;
+      if (slot < kVsMirror) rg[kVsRing + slot] = v;
+    }
+  };
+  const int b_top = (nhi - 1) / A;
+  const int b_bot = nlo / A;
+
+  double acc[A];
+#pragma unroll
+  for (int u = 0; u < A; ++u) acc[u] = 0.0;
+  double ch[C > 0 ? C : 1][A];
+#pragma unroll
+  for (int k = 0; k < (C > 0 ? C : 1); ++k)
+#pragma unroll
+    for (int u = 0; u < A; ++u) ch[k][u] = 0.0;
+
+  // ---- output rows: parked in registers nothing else uses and stored at the next chunk boundary,
+  // right after the ring commit and before the next prefetch.  A VMEM store's data registers must
+  // not be rewritten before the store completes (vmcnt, in order with the prefetch loads), so storing
+  // from reused registers would put a wait for the prefetch at the head of every block.
+  constexpr int P = C == 0 ? 2 : 1;
+  double* const outb = kind == 0 ? rlow : (kind == 1 ? rup : rflat);
+  double pend[P][A];
+  int64_t prow[P];
+  int npend = 0;
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    prow[i] = 0;
+#pragma unroll
+    for (int u = 0; u < A; ++u) pend[i][u] = 0.0;
+  }
+  auto flush = [&]() {
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      if (i < npend) {
+        double* o = outb + prow[i];
+#pragma unroll
+        for (int u = 0; u < A; ++u)
+          if (fvalid && A * l + u < nlags) o[A * l + u] = pend[i][u];
+      }
+    }
+    npend = 0;
+  };
+  auto push = [&](const double (&v)[A], double K, int band) {
+    if (npend == P) flush();
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      if (i == npend) {
+#pragma unroll
+        for (int u = 0; u < A; ++u) pend[i][u] = K * v[u];
+        prow[i] = ((int64_t)f * B + band) * nlags;
+      }
+    }
+    ++npend;
+  };
+
+  // chunks [lo_loaded, lo_loaded + 512) resident; the top block needs up to A b_top + 17 A - 2
+  int lo_loaded = ((A * b_top + 17 * A - 1 + kVsChunk - 1) / kVsChunk) * kVsChunk;
+  issue(lo_loaded - kVsChunk);
+  auto ensure = [&](int n0) {
+    while (n0 < lo_loaded) {  // wave-uniform
+      lo_loaded -= kVsChunk;
+      commit(lo_loaded);
+      flush();
+      issue(lo_loaded - kVsChunk);
+      wave_lds_sync();
+    }
+  };
+  ensure(A * b_top);  // stages [lo_loaded, initial lo_loaded), which covers the top block's window
+
+  // ---- events (wave-uniform) ------------------------------------------------------------------
+  const int nev = kind == 2 ? c.fl_nev : B;
+  int k = 0;
+  // event records are read with scalar loads: the index is wave-uniform, readfirstlane says so (a
+  // vector load here would wait for the outstanding prefetch at every event)
+  auto ev_S = [&](int kk) -> int {
+    kk = __builtin_amdgcn_readfirstlane(kk);
+    if (kk >= nev) return -1;
+    return kind == 2 ? fev[kk].S : snaps[__builtin_amdgcn_readfirstlane(kind * B + kk)].S;
+  };
+  int evS = ev_S(0);
+  // all events at position S (positions >= S consumed)
+  auto handle_at = [&](int S) {
+    if constexpr (C > 0) {  // flat: fold the positions since the last event into every chain
+#pragma unroll
+      for (int cc = 0; cc < C; ++cc)
+#pragma unroll
+        for (int u = 0; u < A; ++u) ch[cc][u] += acc[u];
+#pragma unroll
+      for (int u = 0; u < A; ++u) acc[u] = 0.0;
+    }
+    while (evS == S) {
+      if constexpr (C > 0) {
+        const FlatEv e = fev[__builtin_amdgcn_readfirstlane(k)];
+#pragma unroll
+        for (int cc = 0; cc < C; ++cc) {
+          if (cc == e.chain) {
+            if (e.type == 1) push(ch[cc], 1.0, e.band);
+#pragma unroll
+            for (int u = 0; u < A; ++u) ch[cc][u] = e.type == 0 ? 0.0 : ch[cc][u];
+          }
+        }
+      } else {
+        const SkSnap e = snaps[__builtin_amdgcn_readfirstlane(kind * B + k)];
+        push(acc, e.K, e.band);
+      }
+      ++k;
+      evS = ev_S(k);
+    }
+  };
+
+  // one block [n0, n0 + A): positions at or above a pending event are consumed first (masked pass),
+  // then the event is handled; usually a single unmasked pass
+  auto block = [&](int n0, double (&lo)[A], const double (&hi)[A]) {
+    ensure(n0);
+    const int base = (n0 + A * l) & (kVsRing - 1);
+#pragma unroll
+    for (int q = 0; q < A; ++q) lo[q] = rg[base + q];
+    const double cur = rg[(n0 + l) & (kVsRing - 1)];
+    const int pos = n0 + l;
+    int hi_m = min(n0 + A, nhi);
+    for (;;) {
+      while (evS >= hi_m) handle_at(evS);
+      const int lo_m = max(max(evS, n0), nlo);
+      vs_fma_block<A>(acc, (pos >= lo_m && pos < hi_m) ? cur : 0.0, lo, hi);
+      if (lo_m <= n0 || lo_m <= nlo) break;
+      hi_m = lo_m;
+    }
+  };
+
+  double X[A], Y[A];
+  {
+    const int base = (A * b_top + A + A * l) & (kVsRing - 1);
+#pragma unroll
+    for (int q = 0; q < A; ++q) Y[q] = rg[base + q];
+  }
+  for (int b = b_top; b >= b_bot;) {
+    block(A * b, X, Y);
+    if (--b < b_bot) break;
+    block(A * b, Y, X);
+    --b;
+  }
+  while (k < nev) handle_at(evS);
+  flush();
+  // keep the parked rows' registers reserved for the whole sweep (see above)
+#pragma unroll
+  for (int i = 0; i < P; ++i)
+#pragma unroll
+    for (int u = 0; u < A; ++u) asm volatile("" ::"v"(pend[i][u]));
 }
 
 template <int NT>
@@ -1720,9 +1998,61 @@ hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* 
   return launch_autocorr_any(c, dct, dense, items, r, nullptr, nullptr, s);
 }
 
+int vsweep_lanes_lags(int nlags) {
+  const int a = (nlags + 15) / 16;
+  for (int v : {4, 8, 10, 12, 16})
+    if (a <= v) return v;
+  return 0;
+}
+int vsweep_chains(int C) {
+  for (int v : {4, 5, 6, 8})
+    if (C <= v) return v;
+  return 0;
+}
+
+template <int A, int C>
+static hipError_t launch_vsweep_ac(const DevConsts& c, const double* dct, int nframes, double* r, double* rup,
+                                   double* rflat, hipStream_t s) {
+  const int ngroups = (nframes + 3) / 4;
+  hipLaunchKernelGGL((ac_vsweep_kernel<A, 0>), dim3(xcd_grid(2 * ngroups)), dim3(64), 0, s, c, dct, r, rup, rflat,
+                     c.sk_snap, c.fl_ev, nframes, ngroups);
+  hipLaunchKernelGGL((ac_vsweep_kernel<A, C>), dim3(xcd_grid(ngroups)), dim3(64), 0, s, c, dct, r, rup, rflat,
+                     c.sk_snap, c.fl_ev, nframes, ngroups);
+  return hipGetLastError();
+}
+template <int A>
+static hipError_t launch_vsweep_a(const DevConsts& c, const double* dct, int nframes, double* r, double* rup,
+                                  double* rflat, hipStream_t s) {
+  switch (vsweep_chains(c.fl_C)) {
+    case 4: return launch_vsweep_ac<A, 4>(c, dct, nframes, r, rup, rflat, s);
+    case 5: return launch_vsweep_ac<A, 5>(c, dct, nframes, r, rup, rflat, s);
+    case 6: return launch_vsweep_ac<A, 6>(c, dct, nframes, r, rup, rflat, s);
+    case 8: return launch_vsweep_ac<A, 8>(c, dct, nframes, r, rup, rflat, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+static hipError_t launch_vsweep(const DevConsts& c, const double* dct, int nframes, double* r, double* rup,
+                                double* rflat, hipStream_t s) {
+  switch (vsweep_lanes_lags(c.nlags)) {
+    case 4: return launch_vsweep_a<4>(c, dct, nframes, r, rup, rflat, s);
+    case 8: return launch_vsweep_a<8>(c, dct, nframes, r, rup, rflat, s);
+    case 10: return launch_vsweep_a<10>(c, dct, nframes, r, rup, rflat, s);
+    case 12: return launch_vsweep_a<12>(c, dct, nframes, r, rup, rflat, s);
+    case 16: return launch_vsweep_a<16>(c, dct, nframes, r, rup, rflat, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 template <int NT>
 static hipError_t launch_struct_nt(const DevConsts& c, const double* dct, int nframes, double* r, double* rup,
-                                   hipStream_t s) {
+                                   double* rflat, hipStream_t s) {
+  if (rflat) {  // lag-parallel VALU sweeps (flat tops included) + straddles
+    const hipError_t e = launch_vsweep(c, dct, nframes, r, rup, rflat, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((ac_band_kernel<NT, true>), dim3(xcd_grid(nframes * c.B)), dim3(64), 0, s, c, dct, r, rup,
+                       rflat, nframes * c.B);
+    return hipGetLastError();
+  }
   static const bool full = getenv("FDLP_SWEEP_FULL_EPI") != nullptr;
   static const bool nosnap = getenv("FDLP_SWEEP_NOSNAP") != nullptr;  // timing experiment only
   const size_t tab = sizeof(SkSnap) * (size_t)c.B;
@@ -1734,16 +2064,18 @@ static hipError_t launch_struct_nt(const DevConsts& c, const double* dct, int nf
     hipLaunchKernelGGL((ac_sweep_kernel<NT, 64>), dim3(xcd_grid(2 * nframes)), dim3(64), tab, s, c, dct, r, rup, 2 * nframes);
   else
     hipLaunchKernelGGL((ac_sweep_kernel<NT, 32>), dim3(xcd_grid(2 * nframes)), dim3(64), tab, s, c, dct, r, rup, 2 * nframes);
-  hipLaunchKernelGGL(ac_band_kernel<NT>, dim3(xcd_grid(nframes * c.B)), dim3(64), 0, s, c, dct, r, rup, nframes * c.B);
+  hipLaunchKernelGGL((ac_band_kernel<NT, false>), dim3(xcd_grid(nframes * c.B)), dim3(64), 0, s, c, dct, r, rup,
+                     nullptr, nframes * c.B);
   return hipGetLastError();
 }
 
 hipError_t launch_autocorr_structured(const DevConsts& c, const double* dct, int nframes, double* r,
-                                      double* rup, hipStream_t s) {
+                                      double* rup, double* rflat, hipStream_t s) {
   if (nframes <= 0) return hipSuccess;
   if (!c.sk_e || !c.sk_snap || !c.sk_reg) return hipErrorInvalidValue;
+  if (rflat && !c.fl_ev) return hipErrorInvalidValue;
   switch (autocorr_tiles(c.nlags)) {
-#define FDLP_ST_CASE(n) case n: return launch_struct_nt<n>(c, dct, nframes, r, rup, s);
+#define FDLP_ST_CASE(n) case n: return launch_struct_nt<n>(c, dct, nframes, r, rup, rflat, s);
     FDLP_ST_CASE(1) FDLP_ST_CASE(2) FDLP_ST_CASE(3) FDLP_ST_CASE(4) FDLP_ST_CASE(5)
     FDLP_ST_CASE(6) FDLP_ST_CASE(7) FDLP_ST_CASE(8) FDLP_ST_CASE(9) FDLP_ST_CASE(10)
     FDLP_ST_CASE(11) FDLP_ST_CASE(12) FDLP_ST_CASE(13) FDLP_ST_CASE(14) FDLP_ST_CASE(15)

@@ -112,7 +112,53 @@ struct SkirtTables {
   std::vector<fdlp::SkSnap> snap;  // [2, B] in sweep order
   std::vector<int2> reg;    // [B]
   int smin[2] = {0, 0};
+  // flat-top sweep of ac_vsweep_kernel: events and chain count (C = 0: not possible)
+  std::vector<fdlp::FlatEv> fl;
+  int fl_C = 0, fl_lo = 0, fl_hi = 0;
 };
+
+// Events of the flat-top sweep: band j restarts chain j mod C at m2_j and emits it at m1_j.  Order:
+// S descending; at equal S bands descending (band j emits before band j - C restarts) and a band's
+// restart before its own emission.  C is the smallest count for which no chain is restarted while
+// it still serves a band (checked by replaying the events).
+void flat_events(SkirtTables* T, int B) {
+  T->fl_C = 0;
+  T->fl.clear();
+  T->fl_lo = INT32_MAX;
+  T->fl_hi = 0;
+  for (int j = 0; j < B; ++j) {
+    T->fl_lo = std::min(T->fl_lo, T->reg[j].x);
+    T->fl_hi = std::max(T->fl_hi, T->reg[j].y);
+  }
+  for (int C = 1; C <= 8; ++C) {
+    std::vector<fdlp::FlatEv> ev;
+    for (int j = 0; j < B; ++j) {
+      ev.push_back(fdlp::FlatEv{T->reg[j].y, j, 0, j % C});
+      ev.push_back(fdlp::FlatEv{T->reg[j].x, j, 1, j % C});
+    }
+    std::sort(ev.begin(), ev.end(), [](const fdlp::FlatEv& a, const fdlp::FlatEv& b) {
+      if (a.S != b.S) return a.S > b.S;
+      if (a.band != b.band) return a.band > b.band;
+      return a.type < b.type;
+    });
+    std::vector<int> owner(C, -1);
+    bool ok = true;
+    for (const auto& e : ev) {
+      if (e.type == 0) {
+        if (owner[e.chain] != -1) { ok = false; break; }
+        owner[e.chain] = e.band;
+      } else {
+        if (owner[e.chain] != e.band) { ok = false; break; }
+        owner[e.chain] = -1;
+      }
+    }
+    if (ok) {
+      T->fl = ev;
+      T->fl_C = C;
+      return;
+    }
+  }
+}
 
 bool skirt_tables(const fdlp_config& c, int B, int N, int nfft, SkirtTables* T) {
   if (c.fbank_kind != FDLP_FBANK_COCHLEAR || c.fixed != 1) return false;
@@ -165,6 +211,7 @@ bool skirt_tables(const fdlp_config& c, int B, int N, int nfft, SkirtTables* T) 
     for (int j = 0; j < B; ++j) T->snap[(size_t)sk * B + j] = t[j];
     T->smin[sk] = t[B - 1].S;
   }
+  flat_events(T, B);
   return true;
 }
 
@@ -253,9 +300,11 @@ struct fdlp_plan {
   hipStream_t aux_stream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool sk_avail = false;             // structured autocorrelation possible for this filterbank
-  int ac_path = FDLP_AC_DIRECT;      // FDLP_AC_DIRECT or FDLP_AC_STRUCTURED
+  int ac_path = FDLP_AC_DIRECT;      // FDLP_AC_DIRECT, FDLP_AC_STRUCTURED or FDLP_AC_STRUCTURED_MFMA
+  bool vs_avail = false;             // lag-parallel VALU sweeps possible (flat chains, lag count)
   SkirtTables sk;
-  double *d_sk_e = nullptr, *r_up = nullptr;
+  double *d_sk_e = nullptr, *r_up = nullptr, *r_flat = nullptr;
+  fdlp::FlatEv* d_fl_ev = nullptr;
   fdlp::SkSnap* d_sk_snap = nullptr;
   int2* d_sk_reg = nullptr;
   // modulation-spectrum mode (computeModulationSpectrum.py)
@@ -297,7 +346,7 @@ int free_plan(fdlp_plan* p) {
   void* devs[] = {p->d_fbank, p->d_hamming, p->d_weights, p->d_env_cos, p->d_env_win, p->d_tw1, p->d_post, p->d_rtw,
                   p->d_om1, p->d_om2, p->d_lo, p->d_hi, p->ws.z, p->ws.dct, p->ws.r, p->ws.a, p->ws.gg,
                   p->ws.cep, p->ws.env, p->d_frames, p->d_utts, p->d_sk_e, p->r_up, p->d_sk_snap,
-                  p->d_sk_reg, p->d_faxis};
+                  p->d_sk_reg, p->d_faxis, p->r_flat, p->d_fl_ev};
   for (void* d : devs)
     if (d) (void)hipFree(d);
   if (p->h_frames) (void)hipHostFree(p->h_frames);
@@ -459,7 +508,11 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   }
 
   p->sk_avail = skirt_tables(c, p->B, p->N, p->nfft, &p->sk);
-  p->ac_path = p->sk_avail && getenv("FDLP_AUTOCORR_DIRECT") == nullptr ? FDLP_AC_STRUCTURED : FDLP_AC_DIRECT;
+  p->vs_avail = p->sk_avail && p->sk.fl_C > 0 && fdlp::vsweep_chains(p->sk.fl_C) > 0 &&
+                fdlp::vsweep_lanes_lags(p->nlags) > 0;
+  p->ac_path = !p->sk_avail || getenv("FDLP_AUTOCORR_DIRECT") ? FDLP_AC_DIRECT
+               : (p->vs_avail && !getenv("FDLP_SWEEP_MFMA")) ? FDLP_AC_STRUCTURED
+                                                              : FDLP_AC_STRUCTURED_MFMA;
   if (const char* e = getenv("FDLP_PIPELINE")) p->pipeline = std::max(1, atoi(e));
 
   // modulation weights (:94-118)
@@ -564,6 +617,11 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
     PLAN_TRY(upload(&p->d_sk_reg, p->sk.reg.data(), p->sk.reg.size()));
     d.sk_e = p->d_sk_e; d.sk_snap = p->d_sk_snap; d.sk_reg = p->d_sk_reg;
     d.sk_min[0] = p->sk.smin[0]; d.sk_min[1] = p->sk.smin[1];
+    if (p->vs_avail) {
+      PLAN_TRY(upload(&p->d_fl_ev, p->sk.fl.data(), p->sk.fl.size()));
+      d.fl_ev = p->d_fl_ev; d.fl_nev = (int)p->sk.fl.size(); d.fl_C = p->sk.fl_C;
+      d.fl_lo = p->sk.fl_lo; d.fl_hi = p->sk.fl_hi;
+    }
   }
 
   // workspace
@@ -577,6 +635,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
       hipMalloc((void**)&p->ws.cep, sizeof(double) * items * M) != hipSuccess ||
       hipMalloc((void**)&p->ws.env, sizeof(double) * items * p->kk) != hipSuccess ||
       (p->sk_avail && hipMalloc((void**)&p->r_up, sizeof(double) * items * p->nlags) != hipSuccess) ||
+      (p->vs_avail && hipMalloc((void**)&p->r_flat, sizeof(double) * items * p->nlags) != hipSuccess) ||
       hipMalloc((void**)&p->d_frames, sizeof(fdlp::FrameDesc) * F) != hipSuccess ||
       hipMalloc((void**)&p->d_utts, sizeof(fdlp::UttDesc) * F) != hipSuccess ||
       hipHostMalloc((void**)&p->h_frames, sizeof(fdlp::FrameDesc) * F, hipHostMallocDefault) != hipSuccess ||
@@ -753,8 +812,9 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     HIP_TRY(mark(1));
     HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z + f0 * p->nfft_c, n, p->ws.dct + f0 * N, p->d_om2, st));
     HIP_TRY(mark(2));
-    if (p->ac_path == FDLP_AC_STRUCTURED) {
-      HIP_TRY(fdlp::launch_autocorr_structured(p->dc, p->ws.dct + f0 * N, n, r, p->r_up + it0 * nl, st));
+    if (p->ac_path == FDLP_AC_STRUCTURED || p->ac_path == FDLP_AC_STRUCTURED_MFMA) {
+      double* rflat = p->ac_path == FDLP_AC_STRUCTURED ? p->r_flat + it0 * nl : nullptr;
+      HIP_TRY(fdlp::launch_autocorr_structured(p->dc, p->ws.dct + f0 * N, n, r, p->r_up + it0 * nl, rflat, st));
     } else if (p->fused && !p->debug_intermediates && !p->modspec) {
       // autocorrelation + LPC tail in one launch (stage 3 is then empty)
       HIP_TRY(fdlp::launch_band_fused(p->dc, p->cfg.odd_mod_zero, p->ws.dct + f0 * N, its, r, env, st));
@@ -804,13 +864,13 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
 int fdlp_set_autocorr_path(fdlp_plan* p, int32_t path) {
   if (!p) return fail(FDLP_E_INVALID, "fdlp_set_autocorr_path: null plan");
   if (path == FDLP_AC_AUTO) {
-    p->ac_path = p->sk_avail ? FDLP_AC_STRUCTURED : FDLP_AC_DIRECT;
+    p->ac_path = !p->sk_avail ? FDLP_AC_DIRECT : (p->vs_avail ? FDLP_AC_STRUCTURED : FDLP_AC_STRUCTURED_MFMA);
   } else if (path == FDLP_AC_DIRECT) {
     p->ac_path = FDLP_AC_DIRECT;
-  } else if (path == FDLP_AC_STRUCTURED) {
+  } else if (path == FDLP_AC_STRUCTURED || path == FDLP_AC_STRUCTURED_MFMA) {
     if (!p->sk_avail)
       return fail(FDLP_E_INVALID, "structured autocorrelation needs the cochlear filterbank with fixed=1");
-    p->ac_path = FDLP_AC_STRUCTURED;
+    p->ac_path = (path == FDLP_AC_STRUCTURED && p->vs_avail) ? FDLP_AC_STRUCTURED : FDLP_AC_STRUCTURED_MFMA;
   } else {
     return fail(FDLP_E_INVALID, "fdlp_set_autocorr_path: unknown path");
   }

@@ -237,7 +237,7 @@ class FdlpPlan:
         check(lib.fdlp_compute(self._h, ctypes.byref(b), ctypes.c_void_p(s.cuda_stream)))
         return out[:total], rows, out64
 
-    AUTOCORR_PATHS = {"auto": 0, "direct": 1, "structured": 2}
+    AUTOCORR_PATHS = {"auto": 0, "direct": 1, "structured": 2, "structured_mfma": 3}
 
     @property
     def autocorr_path(self) -> str:
@@ -245,7 +245,7 @@ class FdlpPlan:
         skirt-factorised algorithm, cochlear filterbank with fixed=1)."""
         v = lib.fdlp_autocorr_path(self._h)
         check(v if v < 0 else 0)
-        return {1: "direct", 2: "structured"}[v]
+        return {1: "direct", 2: "structured", 3: "structured_mfma"}[v]
 
     def set_autocorr_path(self, path: str = "auto"):
         check(lib.fdlp_set_autocorr_path(self._h, self.AUTOCORR_PATHS[path]))

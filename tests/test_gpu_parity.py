@@ -10,11 +10,12 @@ from conftest import GOLDEN_SETS, feature_cfg, load_golden, oracle_cfg
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
-# 'short2' is a 2-sample utterance: reflect padding turns it into a near-constant sequence whose
-# band energies outside DC sit at the fp64 rounding floor of the DCT, so any reordering of fp64
-# sums moves its log features by up to ~1e-3 (the oracle's FFT order vs the reference's differs
-# by 2e-5 already).  Every other utterance is held to TOL.
-TOL_UTT = {"short2": 1e-3}
+# 'short2' is a 2-sample utterance: reflect padding turns it into an alternating sequence whose
+# band energies away from DC and Nyquist sit at the fp64 rounding floor of the DCT, so its features
+# are ill-conditioned at the rounding level: perturbing every autocorrelation by 1e-15 r0 (a few
+# ulps of a 24000-term sum) moves them by 1.4e-3 in the oracle (tests/test_oracle_golden.py::
+# test_short2_is_rounding_ill_conditioned).  It is held to 3e-3; every other utterance to TOL.
+TOL_UTT = {"short2": 3e-3}
 
 
 def _batch_inputs(meta, sig, z):
@@ -130,7 +131,7 @@ def test_stage_dct_and_lpc_vs_reference_stages():
             np.testing.assert_allclose(c[i], z["%s_c%d" % (tag, lim)], rtol=1e-9, atol=1e-9)
 
 
-@pytest.mark.parametrize("path", ["structured", "direct"])
+@pytest.mark.parametrize("path", ["structured", "structured_mfma", "direct"])
 def test_intermediates_vs_oracle(path):
     """Every stage of one utterance against the oracle's intermediates."""
     from oracle import fdlp_oracle as O
@@ -153,20 +154,25 @@ STRUCT_CFGS = [
     ("cochlear,0.5,2.5,1,1.5,1", 40, 1.0, 60, 60),   # narrow flat top, steep lower skirt
     ("cochlear,2,0.5,1,4,1.2", 20, 0.5, 30, 40),     # wide flat top, warped axis, short frames
     ("cochlear,1,1,1,2.5,1", 7, 1.5, 238, 100),      # few wide bands, the largest order
+    ("cochlear,0.02,1,1,2.5,1", 30, 0.5, 40, 40),    # (near-)empty flat tops
+    ("cochlear,3,1,1,2.5,1", 60, 0.5, 20, 20),       # wide overlapping flat tops (many chains)
 ]
 
 
+@pytest.mark.parametrize("path", ["structured", "structured_mfma"])
 @pytest.mark.parametrize("fb,nf,fd,order,cn", STRUCT_CFGS)
-def test_structured_autocorr_matches_oracle(fb, nf, fd, order, cn):
+def test_structured_autocorr_matches_oracle(fb, nf, fd, order, cn, path):
     """The skirt-factorised autocorrelation equals the oracle's FFT autocorrelation of every band
     (features.py:223-226) to fp64 rounding, on speech-like and on white input, with the edge bands
-    whose lower skirt (band 0) or upper skirt (last band) is empty."""
+    whose lower skirt (band 0) or upper skirt (last band) is empty; for both the lag-parallel VALU
+    sweeps ('structured') and the MFMA lag-tile sweeps ('structured_mfma')."""
     from oracle import fdlp_oracle as O
     from speech_recognition_tools_amd import FdlpPlan, FeatureConfig, PyRandom
     cfg = FeatureConfig(fbank_type=fb, nfilters=nf, fduration=fd, order=order, coeff_num=cn,
                         coeff_range="0,%d" % cn)
     plan = FdlpPlan(cfg, device=0, max_frames=64)
-    assert plan.autocorr_path == "structured"
+    assert plan.autocorr_path in ("structured", "structured_mfma")
+    plan.set_autocorr_path(path)
     plan.set_debug(True)
     rng = np.random.default_rng(nf + order)
     T = 16000 + 123
