@@ -43,6 +43,9 @@ struct SkSnap {
   double K;
 };
 
+constexpr int kMaxFlatParts = 4;
+constexpr int kMaxChains = 8;
+
 // One event of the flat-top sweep (ac_vsweep_kernel): at sweep position S (after the positions >= S
 // are consumed) restart (type 0) or emit (type 1) chain `chain`, which serves band `band`.
 struct FlatEv {
@@ -73,6 +76,12 @@ struct DevConsts {
   const FlatEv* fl_ev = nullptr;  // [fl_nev] flat-top events sorted by S descending
   int fl_nev = 0, fl_C = 0;       // event count, chains needed (bands j and j - C never overlap)
   int fl_lo = 0, fl_hi = 0;       // min m1, max m2
+  // the flat sweep is split into fl_H position parts [fl_part_lo[h], fl_part_hi[h]) run by different
+  // waves; part h takes the events fl_ev[fl_part_ev[h] .. fl_part_ev[h+1]) and, for h < fl_H - 1, leaves
+  // every chain in rflat_part[f][h][chain] for the bands that continue below it
+  int fl_H = 1;
+  int fl_part_lo[kMaxFlatParts] = {0}, fl_part_hi[kMaxFlatParts] = {0}, fl_part_ev[kMaxFlatParts + 1] = {0};
+  const int2* fl_band = nullptr;  // [B] (chain, bitmask of the parts h < fl_H - 1 it needs a partial from)
 };
 
 }  // namespace fdlp
@@ -98,7 +107,7 @@ hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const 
 hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* dense_rows,
                            int nframes_or_items, double* r, hipStream_t s);
 hipError_t launch_autocorr_structured(const DevConsts& c, const double* dct, int nframes, double* r,
-                                      double* rup, double* rflat, hipStream_t s);
+                                      double* rup, double* rflat, double* rflat_part, hipStream_t s);
 int vsweep_lanes_lags(int nlags);   // lags per lane of ac_vsweep_kernel, 0 = unsupported
 int vsweep_chains(int C);           // chain count instantiated for C needed chains, 0 = unsupported
 hipError_t launch_levinson(const DevConsts& c, const double* r, int items, double* a,

@@ -826,7 +826,8 @@ __global__ __launch_bounds__(64, 2) void ac_sweep_kernel(DevConsts c, const doub
 template <int NT, bool VS>
 __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const double* __restrict__ dct,
                                                         double* __restrict__ r, const double* __restrict__ rup,
-                                                        const double* __restrict__ rflat, int items) {
+                                                        const double* __restrict__ rflat,
+                                                        const double* __restrict__ rpart, int items) {
   static_assert(16 * NT <= kAcChunk, "window halo must fit one chunk");
   constexpr int kEpi = (32 + 31) * 17;                   // diag_blocks<NT, 32> image
   constexpr int kWin = (16 * NT + 63) / 64 * 64;         // A window of a straddle (>= nlags - 1)
@@ -939,7 +940,17 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
   const double* uo = rup + (int64_t)item * nlags;
   if constexpr (VS) {
     const double* fo = rflat + (int64_t)item * nlags;
-    diag_blocks<NT, 32>(acc, xs, nlags, lane, [&](int L, double v) { ro[L] = v + ro[L] + uo[L] + fo[L]; });
+    // partial flat sums of the parts above the one holding m1 (at most kMaxFlatParts - 1)
+    const int2 fb = c.fl_band[j];
+    const double* po[kMaxFlatParts - 1];
+    int np = 0;
+    for (int h = 0; h + 1 < c.fl_H; ++h)
+      if (fb.y >> h & 1) po[np++] = rpart + (((int64_t)f * (c.fl_H - 1) + h) * kMaxChains + fb.x) * nlags;
+    diag_blocks<NT, 32>(acc, xs, nlags, lane, [&](int L, double v) {
+      double fl = fo[L];
+      for (int q = 0; q < np; ++q) fl += po[q][L];
+      ro[L] = v + ro[L] + uo[L] + fl;
+    });
   } else {
     diag_blocks<NT, 32>(acc, xs, nlags, lane, [&](int L, double v) { ro[L] = v + ro[L] + uo[L]; });
   }
@@ -977,7 +988,13 @@ __device__ __forceinline__ double row_bcast(double v) {
 
 constexpr int kVsRing = 512;
 constexpr int kVsMirror = 16;
-constexpr int kVsChunk = 64;
+// positions staged per chunk; the prefetch of the next chunk has to cover the HBM latency under load
+// (64 positions, ~3000 cycles of FMAs, measured too short).  The flat sweep keeps its chains in
+// registers, so it stages 128 at a time to stay at two waves per SIMD.
+template <int A, int C>
+constexpr int vs_chunk() { return (C == 0 && 18 * A < kVsRing - 256) ? 256 : 128; }
+template <int C>
+constexpr int vs_waves_per_simd() { return 2; }
 
 template <int A, int V = 0>
 __device__ __forceinline__ void vs_bcast_all(double (&bb)[A], double cur) {
@@ -999,22 +1016,27 @@ __device__ __forceinline__ void vs_fma_block(double (&acc)[A], double cur, const
 }
 
 template <int A, int C>
-__global__ __launch_bounds__(64, 2) void ac_vsweep_kernel(DevConsts c, const double* __restrict__ dct,
+__global__ __launch_bounds__(64, vs_waves_per_simd<C>()) void ac_vsweep_kernel(DevConsts c, const double* __restrict__ dct,
                                                           double* __restrict__ rlow, double* __restrict__ rup,
                                                           double* __restrict__ rflat,
+                                                          double* __restrict__ rpart,
                                                           const SkSnap* __restrict__ snaps,
                                                           const FlatEv* __restrict__ fev, int nframes,
                                                           int ngroups) {
   // snaps / fev (= c.sk_snap / c.fl_ev) as restrict parameters: not clobbered by the output stores,
   // so their wave-uniform reads become scalar loads
+  constexpr int kVsChunk = vs_chunk<A, C>();
   static_assert(A % 2 == 0 && A <= 16 && 18 * A < kVsRing - kVsChunk && A <= kVsMirror + 1, "vsweep geometry");
   __shared__ double ring_all[4][kVsRing + kVsMirror];
   // C == 0: the two skirt sweeps, item = 2 group + skirt (a frame group's two sweeps adjacent on one
   // XCD, so its D rows are read from HBM once); C > 0: the flat-top sweep, item = group
+  // (C > 0: item = H group + part, the parts of a frame group adjacent on one XCD)
+  const int H = C == 0 ? 2 : c.fl_H;
   const int item = xcd_item();
-  if (item >= (C == 0 ? 2 : 1) * ngroups) return;
-  const int g = C == 0 ? item >> 1 : item;
-  const int kind = C == 0 ? (item & 1) : 2;
+  if (item >= H * ngroups) return;
+  const int g = item / H;
+  const int part = item - H * g;
+  const int kind = C == 0 ? part : 2;
   const int lane = threadIdx.x;
   const int row = lane >> 4;
   const int l = lane & 15;
@@ -1024,11 +1046,23 @@ __global__ __launch_bounds__(64, 2) void ac_vsweep_kernel(DevConsts c, const dou
   const double* drow = dct + (int64_t)(fvalid ? f : 0) * N;
   const double* ew = c.sk_e + (int64_t)(kind == 1 ? N : 0);
   double* rg = ring_all[row];
-  const int nlo = kind == 2 ? c.fl_lo : c.sk_min[kind];
-  const int nhi = kind == 2 ? c.fl_hi : N;
+  const int nlo = kind == 2 ? c.fl_part_lo[part] : c.sk_min[kind];
+  const int nhi = kind == 2 ? c.fl_part_hi[part] : N;
+  const int kbeg = kind == 2 ? c.fl_part_ev[part] : 0;
+  const int kend = kind == 2 ? c.fl_part_ev[part + 1] : B;
+  // chains left for the parts below (flat, part < H - 1)
+  auto part_store = [&](auto&& value) {
+    if (kind == 2 && part < H - 1) {
+      for (int cc = 0; cc < C; ++cc) {
+        double* o = rpart + (((int64_t)f * (H - 1) + part) * kMaxChains + cc) * nlags;
+#pragma unroll
+        for (int u = 0; u < A; ++u)
+          if (fvalid && A * l + u < nlags) o[A * l + u] = value(cc, u);
+      }
+    }
+  };
   if (nhi <= nlo) {  // nothing to sweep: every snapshot / emission is zero
-    const int nev = kind == 2 ? c.fl_nev : B;
-    for (int k = 0; k < nev; ++k) {
+    for (int k = kbeg; k < kend; ++k) {
       const int band = kind == 2 ? fev[k].band : snaps[kind * B + k].band;
       if (kind == 2 && fev[k].type == 0) continue;
       double* o = (kind == 0 ? rlow : (kind == 1 ? rup : rflat)) + ((int64_t)f * B + band) * nlags;
@@ -1036,6 +1070,7 @@ __global__ __launch_bounds__(64, 2) void ac_vsweep_kernel(DevConsts c, const dou
       for (int u = 0; u < A; ++u)
         if (fvalid && A * l + u < nlags) o[A * l + u] = 0.0;
     }
+    part_store([](int, int) { return 0.0; });
     return;
   }
 
@@ -1132,16 +1167,15 @@ __global__ __launch_bounds__(64, 2) void ac_vsweep_kernel(DevConsts c, const dou
   ensure(A * b_top);  // stages [lo_loaded, initial lo_loaded), which covers the top block's window
 
   // ---- events (wave-uniform) ------------------------------------------------------------------
-  const int nev = kind == 2 ? c.fl_nev : B;
-  int k = 0;
+  int k = kbeg;
   // event records are read with scalar loads: the index is wave-uniform, readfirstlane says so (a
   // vector load here would wait for the outstanding prefetch at every event)
   auto ev_S = [&](int kk) -> int {
     kk = __builtin_amdgcn_readfirstlane(kk);
-    if (kk >= nev) return -1;
+    if (kk >= kend) return -1;
     return kind == 2 ? fev[kk].S : snaps[__builtin_amdgcn_readfirstlane(kind * B + kk)].S;
   };
-  int evS = ev_S(0);
+  int evS = ev_S(k);
   // all events at position S (positions >= S consumed)
   auto handle_at = [&](int S) {
     if constexpr (C > 0) {  // flat: fold the positions since the last event into every chain
@@ -1203,8 +1237,17 @@ __global__ __launch_bounds__(64, 2) void ac_vsweep_kernel(DevConsts c, const dou
     block(A * b, Y, X);
     --b;
   }
-  while (k < nev) handle_at(evS);
+  while (k < kend) handle_at(evS);
   flush();
+  if constexpr (C > 0) {
+    part_store([&](int cc, int u) {
+      double v = 0.0;
+#pragma unroll
+      for (int q = 0; q < C; ++q)
+        if (q == cc) v = ch[q][u] + acc[u];
+      return v;
+    });
+  }
   // keep the parked rows' registers reserved for the whole sweep (see above)
 #pragma unroll
   for (int i = 0; i < P; ++i)
@@ -2012,45 +2055,45 @@ int vsweep_chains(int C) {
 
 template <int A, int C>
 static hipError_t launch_vsweep_ac(const DevConsts& c, const double* dct, int nframes, double* r, double* rup,
-                                   double* rflat, hipStream_t s) {
+                                   double* rflat, double* rpart, hipStream_t s) {
   const int ngroups = (nframes + 3) / 4;
   hipLaunchKernelGGL((ac_vsweep_kernel<A, 0>), dim3(xcd_grid(2 * ngroups)), dim3(64), 0, s, c, dct, r, rup, rflat,
-                     c.sk_snap, c.fl_ev, nframes, ngroups);
-  hipLaunchKernelGGL((ac_vsweep_kernel<A, C>), dim3(xcd_grid(ngroups)), dim3(64), 0, s, c, dct, r, rup, rflat,
-                     c.sk_snap, c.fl_ev, nframes, ngroups);
+                     rpart, c.sk_snap, c.fl_ev, nframes, ngroups);
+  hipLaunchKernelGGL((ac_vsweep_kernel<A, C>), dim3(xcd_grid(c.fl_H * ngroups)), dim3(64), 0, s, c, dct, r, rup,
+                     rflat, rpart, c.sk_snap, c.fl_ev, nframes, ngroups);
   return hipGetLastError();
 }
 template <int A>
 static hipError_t launch_vsweep_a(const DevConsts& c, const double* dct, int nframes, double* r, double* rup,
-                                  double* rflat, hipStream_t s) {
+                                  double* rflat, double* rpart, hipStream_t s) {
   switch (vsweep_chains(c.fl_C)) {
-    case 4: return launch_vsweep_ac<A, 4>(c, dct, nframes, r, rup, rflat, s);
-    case 5: return launch_vsweep_ac<A, 5>(c, dct, nframes, r, rup, rflat, s);
-    case 6: return launch_vsweep_ac<A, 6>(c, dct, nframes, r, rup, rflat, s);
-    case 8: return launch_vsweep_ac<A, 8>(c, dct, nframes, r, rup, rflat, s);
+    case 4: return launch_vsweep_ac<A, 4>(c, dct, nframes, r, rup, rflat, rpart, s);
+    case 5: return launch_vsweep_ac<A, 5>(c, dct, nframes, r, rup, rflat, rpart, s);
+    case 6: return launch_vsweep_ac<A, 6>(c, dct, nframes, r, rup, rflat, rpart, s);
+    case 8: return launch_vsweep_ac<A, 8>(c, dct, nframes, r, rup, rflat, rpart, s);
     default: return hipErrorInvalidValue;
   }
 }
 static hipError_t launch_vsweep(const DevConsts& c, const double* dct, int nframes, double* r, double* rup,
-                                double* rflat, hipStream_t s) {
+                                double* rflat, double* rpart, hipStream_t s) {
   switch (vsweep_lanes_lags(c.nlags)) {
-    case 4: return launch_vsweep_a<4>(c, dct, nframes, r, rup, rflat, s);
-    case 8: return launch_vsweep_a<8>(c, dct, nframes, r, rup, rflat, s);
-    case 10: return launch_vsweep_a<10>(c, dct, nframes, r, rup, rflat, s);
-    case 12: return launch_vsweep_a<12>(c, dct, nframes, r, rup, rflat, s);
-    case 16: return launch_vsweep_a<16>(c, dct, nframes, r, rup, rflat, s);
+    case 4: return launch_vsweep_a<4>(c, dct, nframes, r, rup, rflat, rpart, s);
+    case 8: return launch_vsweep_a<8>(c, dct, nframes, r, rup, rflat, rpart, s);
+    case 10: return launch_vsweep_a<10>(c, dct, nframes, r, rup, rflat, rpart, s);
+    case 12: return launch_vsweep_a<12>(c, dct, nframes, r, rup, rflat, rpart, s);
+    case 16: return launch_vsweep_a<16>(c, dct, nframes, r, rup, rflat, rpart, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 template <int NT>
 static hipError_t launch_struct_nt(const DevConsts& c, const double* dct, int nframes, double* r, double* rup,
-                                   double* rflat, hipStream_t s) {
+                                   double* rflat, double* rpart, hipStream_t s) {
   if (rflat) {  // lag-parallel VALU sweeps (flat tops included) + straddles
-    const hipError_t e = launch_vsweep(c, dct, nframes, r, rup, rflat, s);
+    const hipError_t e = launch_vsweep(c, dct, nframes, r, rup, rflat, rpart, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((ac_band_kernel<NT, true>), dim3(xcd_grid(nframes * c.B)), dim3(64), 0, s, c, dct, r, rup,
-                       rflat, nframes * c.B);
+                       rflat, rpart, nframes * c.B);
     return hipGetLastError();
   }
   static const bool full = getenv("FDLP_SWEEP_FULL_EPI") != nullptr;
@@ -2065,17 +2108,17 @@ static hipError_t launch_struct_nt(const DevConsts& c, const double* dct, int nf
   else
     hipLaunchKernelGGL((ac_sweep_kernel<NT, 32>), dim3(xcd_grid(2 * nframes)), dim3(64), tab, s, c, dct, r, rup, 2 * nframes);
   hipLaunchKernelGGL((ac_band_kernel<NT, false>), dim3(xcd_grid(nframes * c.B)), dim3(64), 0, s, c, dct, r, rup,
-                     nullptr, nframes * c.B);
+                     nullptr, nullptr, nframes * c.B);
   return hipGetLastError();
 }
 
 hipError_t launch_autocorr_structured(const DevConsts& c, const double* dct, int nframes, double* r,
-                                      double* rup, double* rflat, hipStream_t s) {
+                                      double* rup, double* rflat, double* rpart, hipStream_t s) {
   if (nframes <= 0) return hipSuccess;
   if (!c.sk_e || !c.sk_snap || !c.sk_reg) return hipErrorInvalidValue;
-  if (rflat && !c.fl_ev) return hipErrorInvalidValue;
+  if (rflat && (!c.fl_ev || !c.fl_band || (c.fl_H > 1 && !rpart))) return hipErrorInvalidValue;
   switch (autocorr_tiles(c.nlags)) {
-#define FDLP_ST_CASE(n) case n: return launch_struct_nt<n>(c, dct, nframes, r, rup, rflat, s);
+#define FDLP_ST_CASE(n) case n: return launch_struct_nt<n>(c, dct, nframes, r, rup, rflat, rpart, s);
     FDLP_ST_CASE(1) FDLP_ST_CASE(2) FDLP_ST_CASE(3) FDLP_ST_CASE(4) FDLP_ST_CASE(5)
     FDLP_ST_CASE(6) FDLP_ST_CASE(7) FDLP_ST_CASE(8) FDLP_ST_CASE(9) FDLP_ST_CASE(10)
     FDLP_ST_CASE(11) FDLP_ST_CASE(12) FDLP_ST_CASE(13) FDLP_ST_CASE(14) FDLP_ST_CASE(15)

@@ -115,7 +115,39 @@ struct SkirtTables {
   // flat-top sweep of ac_vsweep_kernel: events and chain count (C = 0: not possible)
   std::vector<fdlp::FlatEv> fl;
   int fl_C = 0, fl_lo = 0, fl_hi = 0;
+  int fl_H = 1;
+  int part_lo[fdlp::kMaxFlatParts] = {0}, part_hi[fdlp::kMaxFlatParts] = {0}, part_ev[fdlp::kMaxFlatParts + 1] = {0};
+  std::vector<int2> fl_band;  // [B] (chain, partial-part mask)
 };
+
+// Split the flat sweep [fl_lo, fl_hi) into H equal position parts (more waves: the flat sweep has one
+// unit per frame against two for the skirts).  Part h covers [P_{h+1}, P_h) and takes the events with
+// P_{h+1} <= S < P_h (part 0 also S = fl_hi).  Band j needs the partial chain of part h when its flat top
+// crosses the part's lower end: m1_j < P_{h+1} < m2_j.
+void flat_parts(SkirtTables* T, int B, int H) {
+  if (T->fl_hi - T->fl_lo < 1024 * H) H = 1;
+  T->fl_H = H;
+  std::vector<int> P(H + 1);
+  for (int h = 0; h <= H; ++h) P[h] = T->fl_hi - (int)((int64_t)(T->fl_hi - T->fl_lo) * h / H);
+  for (int h = 0; h < H; ++h) { T->part_hi[h] = P[h]; T->part_lo[h] = P[h + 1]; }
+  const int nev = (int)T->fl.size();
+  T->part_ev[0] = 0;
+  for (int h = 1; h <= H; ++h) {
+    int k = T->part_ev[h - 1];
+    if (h == H) k = nev;
+    else while (k < nev && T->fl[k].S >= P[h]) ++k;
+    T->part_ev[h] = k;
+  }
+  T->fl_band.assign(B, make_int2(0, 0));
+  for (int j = 0; j < B; ++j) {
+    int mask = 0;
+    for (int h = 0; h + 1 < H; ++h)
+      if (T->reg[j].x < P[h + 1] && P[h + 1] < T->reg[j].y) mask |= 1 << h;
+    T->fl_band[j] = make_int2(j % std::max(T->fl_C, 1), mask);
+  }
+}
+
+void flat_parts(SkirtTables* T, int B, int H);
 
 // Events of the flat-top sweep: band j restarts chain j mod C at m2_j and emits it at m1_j.  Order:
 // S descending; at equal S bands descending (band j emits before band j - C restarts) and a band's
@@ -155,6 +187,7 @@ void flat_events(SkirtTables* T, int B) {
     if (ok) {
       T->fl = ev;
       T->fl_C = C;
+      flat_parts(T, B, getenv("FDLP_FLAT_PARTS") ? std::max(1, std::min(fdlp::kMaxFlatParts, atoi(getenv("FDLP_FLAT_PARTS")))) : 2);
       return;
     }
   }
@@ -303,8 +336,9 @@ struct fdlp_plan {
   int ac_path = FDLP_AC_DIRECT;      // FDLP_AC_DIRECT, FDLP_AC_STRUCTURED or FDLP_AC_STRUCTURED_MFMA
   bool vs_avail = false;             // lag-parallel VALU sweeps possible (flat chains, lag count)
   SkirtTables sk;
-  double *d_sk_e = nullptr, *r_up = nullptr, *r_flat = nullptr;
+  double *d_sk_e = nullptr, *r_up = nullptr, *r_flat = nullptr, *r_flat_part = nullptr;
   fdlp::FlatEv* d_fl_ev = nullptr;
+  int2* d_fl_band = nullptr;
   fdlp::SkSnap* d_sk_snap = nullptr;
   int2* d_sk_reg = nullptr;
   // modulation-spectrum mode (computeModulationSpectrum.py)
@@ -346,7 +380,7 @@ int free_plan(fdlp_plan* p) {
   void* devs[] = {p->d_fbank, p->d_hamming, p->d_weights, p->d_env_cos, p->d_env_win, p->d_tw1, p->d_post, p->d_rtw,
                   p->d_om1, p->d_om2, p->d_lo, p->d_hi, p->ws.z, p->ws.dct, p->ws.r, p->ws.a, p->ws.gg,
                   p->ws.cep, p->ws.env, p->d_frames, p->d_utts, p->d_sk_e, p->r_up, p->d_sk_snap,
-                  p->d_sk_reg, p->d_faxis, p->r_flat, p->d_fl_ev};
+                  p->d_sk_reg, p->d_faxis, p->r_flat, p->d_fl_ev, p->r_flat_part, p->d_fl_band};
   for (void* d : devs)
     if (d) (void)hipFree(d);
   if (p->h_frames) (void)hipHostFree(p->h_frames);
@@ -621,6 +655,10 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
       PLAN_TRY(upload(&p->d_fl_ev, p->sk.fl.data(), p->sk.fl.size()));
       d.fl_ev = p->d_fl_ev; d.fl_nev = (int)p->sk.fl.size(); d.fl_C = p->sk.fl_C;
       d.fl_lo = p->sk.fl_lo; d.fl_hi = p->sk.fl_hi;
+      PLAN_TRY(upload(&p->d_fl_band, p->sk.fl_band.data(), p->sk.fl_band.size()));
+      d.fl_band = p->d_fl_band; d.fl_H = p->sk.fl_H;
+      for (int h = 0; h < fdlp::kMaxFlatParts; ++h) { d.fl_part_lo[h] = p->sk.part_lo[h]; d.fl_part_hi[h] = p->sk.part_hi[h]; }
+      for (int h = 0; h <= fdlp::kMaxFlatParts; ++h) d.fl_part_ev[h] = p->sk.part_ev[h];
     }
   }
 
@@ -636,6 +674,9 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
       hipMalloc((void**)&p->ws.env, sizeof(double) * items * p->kk) != hipSuccess ||
       (p->sk_avail && hipMalloc((void**)&p->r_up, sizeof(double) * items * p->nlags) != hipSuccess) ||
       (p->vs_avail && hipMalloc((void**)&p->r_flat, sizeof(double) * items * p->nlags) != hipSuccess) ||
+      (p->vs_avail && p->sk.fl_H > 1 &&
+       hipMalloc((void**)&p->r_flat_part, sizeof(double) * F * (p->sk.fl_H - 1) * fdlp::kMaxChains * p->nlags) !=
+           hipSuccess) ||
       hipMalloc((void**)&p->d_frames, sizeof(fdlp::FrameDesc) * F) != hipSuccess ||
       hipMalloc((void**)&p->d_utts, sizeof(fdlp::UttDesc) * F) != hipSuccess ||
       hipHostMalloc((void**)&p->h_frames, sizeof(fdlp::FrameDesc) * F, hipHostMallocDefault) != hipSuccess ||
@@ -814,7 +855,10 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     HIP_TRY(mark(2));
     if (p->ac_path == FDLP_AC_STRUCTURED || p->ac_path == FDLP_AC_STRUCTURED_MFMA) {
       double* rflat = p->ac_path == FDLP_AC_STRUCTURED ? p->r_flat + it0 * nl : nullptr;
-      HIP_TRY(fdlp::launch_autocorr_structured(p->dc, p->ws.dct + f0 * N, n, r, p->r_up + it0 * nl, rflat, st));
+      double* rpart = p->ac_path == FDLP_AC_STRUCTURED && p->r_flat_part
+                          ? p->r_flat_part + (size_t)f0 * (p->sk.fl_H - 1) * fdlp::kMaxChains * nl
+                          : nullptr;
+      HIP_TRY(fdlp::launch_autocorr_structured(p->dc, p->ws.dct + f0 * N, n, r, p->r_up + it0 * nl, rflat, rpart, st));
     } else if (p->fused && !p->debug_intermediates && !p->modspec) {
       // autocorrelation + LPC tail in one launch (stage 3 is then empty)
       HIP_TRY(fdlp::launch_band_fused(p->dc, p->cfg.odd_mod_zero, p->ws.dct + f0 * N, its, r, env, st));
