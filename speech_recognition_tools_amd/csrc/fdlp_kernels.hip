@@ -1003,16 +1003,37 @@ __device__ __forceinline__ void vs_bcast_all(double (&bb)[A], double cur) {
     vs_bcast_all<A, V + 1>(bb, cur);
   }
 }
-// all A broadcasts first (their DPP latency is then hidden behind the FMAs of the earlier ones)
+// acc += s[n0+V] * w with s[n0+V] read from lane V of the row by the FMA itself (DP ALU DPP:
+// v_fmac_f64 takes row_newbcast on its first source), so a block costs A^2 FMAs and no moves
+template <int V>
+__device__ __forceinline__ void fmac_bcast(double& acc, double cur, double w) {
+  asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(cur), "v"(w), "n"(V));
+}
+template <int A, int V = 0>
+__device__ __forceinline__ void vs_fma_rows(double (&acc)[A], double cur, const double (&lo)[A], const double (&hi)[A]) {
+  if constexpr (V < A) {
+#pragma unroll
+    for (int u = 0; u < A; ++u) fmac_bcast<V>(acc[u], cur, (V + u < A) ? lo[V + u] : hi[V + u - A]);
+    vs_fma_rows<A, V + 1>(acc, cur, lo, hi);
+  }
+}
 template <int A>
 __device__ __forceinline__ void vs_fma_block(double (&acc)[A], double cur, const double (&lo)[A],
                                              const double (&hi)[A]) {
+#ifdef FDLP_VSWEEP_DPP_MOV
   double bb[A];
   vs_bcast_all<A>(bb, cur);
 #pragma unroll
   for (int v = 0; v < A; ++v)
 #pragma unroll
     for (int u = 0; u < A; ++u) acc[u] = fma(bb[v], (v + u < A) ? lo[v + u] : hi[v + u - A], acc[u]);
+#else
+  // the DPP source must be two wait states past its VALU write (the compiler cannot see the DPP
+  // inside the asm): copy it through one asm that ends in the wait
+  double cm;
+  asm volatile("v_mov_b64 %0, %1\n\ts_nop 1" : "=v"(cm) : "v"(cur));
+  vs_fma_rows<A>(acc, cm, lo, hi);
+#endif
 }
 
 template <int A, int C>
