@@ -76,7 +76,8 @@ def _latest_pmc():
 
 
 PMC_FILE = _latest_pmc()
-AC_KERNEL_PREFIX = {"structured": ("fdlp::ac_sweep_kernel", "fdlp::ac_band_kernel"),
+AC_KERNEL_PREFIX = {"structured": ("fdlp::ac_vsweep_kernel", "fdlp::ac_band_kernel"),
+                    "structured_mfma": ("fdlp::ac_sweep_kernel", "fdlp::ac_band_kernel"),
                     "direct": ("fdlp::autocorr_kernel",)}
 
 
@@ -88,32 +89,43 @@ def stage_traffic(path):
         rows = json.load(open(PMC_FILE))
     except (OSError, ValueError, TypeError):
         return None
-    tot, seen = 0.0, 0
+    tot, seen = 0.0, set()
     for name, m in rows.items():
         short = name.replace("void ", "")
-        if short.startswith(AC_KERNEL_PREFIX[path]) and "fetch_bytes_x2" in m and "write_bytes" in m:
-            tot += m["fetch_bytes_x2"] + m["write_bytes"]
-            seen += 1
-    return tot if seen == len(AC_KERNEL_PREFIX[path]) else None
+        for pre in AC_KERNEL_PREFIX[path]:
+            if short.startswith(pre) and "fetch_bytes_x2" in m and "write_bytes" in m:
+                tot += m["fetch_bytes_x2"] + m["write_bytes"]
+                seen.add(pre)
+    return tot if len(seen) == len(AC_KERNEL_PREFIX[path]) else None
 
 
-AC_KERNELS = {"structured": "autocorr stage: ac_sweep_kernel + ac_band_kernel (v_mfma_f64_16x16x4f64)",
+AC_KERNELS = {"structured": "autocorr stage: ac_vsweep_kernel x2 (fp64 VALU FMA, lag-parallel sweeps) + "
+                            "ac_band_kernel (v_mfma_f64_16x16x4f64 straddles); the 78.6 TFLOP/s fp64 peak is "
+                            "shared by the VALU and matrix pipes",
+              "structured_mfma": "autocorr stage: ac_sweep_kernel + ac_band_kernel (v_mfma_f64_16x16x4f64)",
               "direct": "autocorr stage: autocorr_kernel (v_mfma_f64_16x16x4f64)"}
 
 
 def autocorr_flops(plan, support):
-    """Useful fp64 FLOPs of the autocorrelation stage per analysis frame (2 per MAC).
-    direct: nlags MACs per tap of every band support (circular).  structured: the two skirt sweeps,
-    the flat tops and the boundary straddles (DESIGN.md "Structured autocorrelation")."""
+    """Useful fp64 FLOPs of the autocorrelation stage per analysis frame (2 per MAC) for the
+    algorithm the path runs.  direct: nlags MACs per tap of every band support (circular).
+    structured_mfma: the two skirt sweeps, the per-band flat tops and the boundary straddles;
+    structured: the same with the flat tops as one sweep over [min m1, max m2) whose products run to N
+    (DESIGN.md "Structured autocorrelation")."""
     nl, N = plan.nlags, plan.N
     lags = np.arange(nl)
     trunc = lambda n: float(np.maximum(n - lags, 0).sum())      # truncated autocorrelation
-    if plan.autocorr_path != "structured":
+    path = plan.autocorr_path
+    if path == "direct":
         return 2.0 * nl * float(support.sum())
     m1, m2 = plan.regions()
     macs = trunc(int(m1.max())) + trunc(N - int(m2.min()))
+    if path == "structured":
+        pos = np.arange(int(m1.min()), int(m2.max()))
+        macs += float(np.minimum(nl, N - pos).sum())
     for j in range(plan.B):
-        macs += trunc(int(m2[j] - m1[j]))
+        if path != "structured":
+            macs += trunc(int(m2[j] - m1[j]))
         for b, lb in ((m1[j], 0), (m2[j], m1[j]), (N, m2[j])):
             macs += float(np.minimum(lags, min(int(b - lb), nl - 1)).sum())
     return 2.0 * macs

@@ -78,19 +78,25 @@ __device__ void stockham_stage(const double2* __restrict__ in, double2* __restri
                                const double2* __restrict__ om, int n, int ncols, int Ns) {
   const int nb = n / R;
   const int total = nb * ncols;
+  const int tw0 = n / (Ns * R);
+  const float inv_ns = 1.0f / (float)Ns;
   for (int b = threadIdx.x; b < total; b += blockDim.x) {
     const int col = b % ncols;
     const int j = b / ncols;
-    const int k = j % Ns;
+    // j / Ns without an integer division (j < 512: the float quotient is off by at most one)
+    int jq = (int)((float)j * inv_ns);
+    jq += (jq + 1) * Ns <= j;
+    jq -= jq * Ns > j;
+    const int k = j - jq * Ns;
     double2 v[R];
-    const int twstep = (n / (Ns * R)) * k;  // omega_{Ns*R}^{k*r} = omega_n^{k*r*n/(Ns*R)}
+    const int twstep = tw0 * k;  // omega_{Ns*R}^{k*r} = omega_n^{k*r*n/(Ns*R)}; twstep * r < n
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       double2 x = in[(j + r * nb) * ncols + col];
-      v[r] = (r == 0) ? x : cmul(x, om[(twstep * r) % n]);
+      v[r] = (r == 0) ? x : cmul(x, om[twstep * r]);
     }
     small_dft<R>(v, om, n);
-    const int idxD = (j / Ns) * Ns * R + k;
+    const int idxD = jq * Ns * R + k;
 #pragma unroll
     for (int r = 0; r < R; ++r) out[(idxD + r * Ns) * ncols + col] = v[r];
   }
@@ -124,9 +130,13 @@ constexpr int kDftCols = 8;     // columns (rows) per workgroup in the two DFT p
 // 1. frames -> Makhoul-reordered real sequence -> column DFTs (length N1) + four-step twiddle
 // -----------------------------------------------------------------------------------------
 __device__ __forceinline__ int64_t reflect_idx(int64_t q, int64_t T) {
-  // numpy 'reflect' pad == periodic reflection with period 2(T-1) (features.py:146)
+  // numpy 'reflect' pad == periodic reflection with period 2(T-1) (features.py:146); the 64-bit
+  // modulo is only needed when the pad exceeds one period (utterances shorter than the padding)
+  if (q >= 0 && q < T) return q;
   if (T == 1) return 0;
   const int64_t P = 2 * (T - 1);
+  if (q < 0 && q > -T) return -q;
+  if (q >= T && q < P) return P - q;
   q %= P;
   if (q < 0) q += P;
   return q < T ? q : P - q;
@@ -273,8 +283,9 @@ __global__ __launch_bounds__(256) void dft2_dct_kernel(DevConsts c, DftPlan d2, 
     const double2 V = res[k2 * kDftCols + row];
     if constexpr (REAL) {
       const int M = N1 * N2;
-      const int km = k == 0 ? 0 : M - k;  // Z_M = Z_0
-      const int k1m = km % N1, k2m = km / N1;
+      // km = M - k (Z_M = Z_0) split as k1m + N1 k2m without a division
+      const int k1m = k1 == 0 ? 0 : N1 - k1;
+      const int k2m = k1 == 0 ? (k2 == 0 ? 0 : N2 - k2) : N2 - 1 - k2;
       const int rm = k1m == k1 ? row : (row < kHalf ? row + kHalf : row - kHalf);
       const double2 W = res[k2m * kDftCols + rm];
       const double2 E = make_double2(0.5 * (V.x + W.x), 0.5 * (V.y - W.y));
@@ -1048,7 +1059,11 @@ __global__ __launch_bounds__(64, vs_waves_per_simd<C>()) void ac_vsweep_kernel(D
   // so their wave-uniform reads become scalar loads
   constexpr int kVsChunk = vs_chunk<A, C>();
   static_assert(A % 2 == 0 && A <= 16 && 18 * A < kVsRing - kVsChunk && A <= kVsMirror + 1, "vsweep geometry");
-  __shared__ double ring_all[4][kVsRing + kVsMirror];
+  // row stride 544 doubles = 17 x 256 B: each ds_read_b128 lane group (lanes 0-3,12-15 of one row and
+  // 4-11 of the next, MI355X_MICROARCH.md LDS) then covers the 64 banks exactly with the 10-double lane
+  // stride of the window reads (A = 10; a 528 stride measured 9.4e7 conflict cycles per launch)
+  __shared__ double ring_all[4][kVsRing + 32];
+  static_assert(kVsMirror <= 32, "mirror fits the row padding");
   // C == 0: the two skirt sweeps, item = 2 group + skirt (a frame group's two sweeps adjacent on one
   // XCD, so its D rows are read from HBM once); C > 0: the flat-top sweep, item = group
   // (C > 0: item = H group + part, the parts of a frame group adjacent on one XCD)
