@@ -144,6 +144,10 @@ def main():
     ap.add_argument("--cpu-per-worker", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pipeline", type=int, default=None, help="sub-batches over two streams (plan default 2)")
+    ap.add_argument("--workload", default="wsj", choices=["wsj", "librispeech"],
+                    help="wsj: --utts utterances of --seconds (BASELINE configs[1]); librispeech: U(1,30) s "
+                         "utterances filling --frames analysis frames per step (configs[4], per GPU)")
+    ap.add_argument("--frames", type=int, default=4096, help="analysis frames per step (librispeech workload)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -171,20 +175,33 @@ def main():
     if args.support_eps is not None:
         cfg.support_eps = args.support_eps
     probe = FdlpPlan(cfg, device=-1)
-    F_u, L_u = probe.geometry(T)
-    frames = F_u * args.utts
+    if args.workload == "wsj":
+        lens = [T] * args.utts
+    else:  # LibriSpeech-960h scale: lengths U(1, 30) s, a fresh draw per rank
+        rs = np.random.RandomState(2000 + rank)
+        lens, fr = [], 0
+        while True:
+            t = int(rs.uniform(1.0, 30.0) * 16000)
+            if fr + probe.geometry(t)[0] > args.frames:
+                break
+            lens.append(t)
+            fr += probe.geometry(t)[0]
+    geo = [probe.geometry(t) for t in lens]
+    frames = sum(g[0] for g in geo)
     plan = FdlpPlan(cfg, device=local, max_frames=frames)
     if args.pipeline is not None:
         plan.set_pipeline(args.pipeline)
     _, lo, hi = probe.fbank()
     support = (hi - lo).astype(np.int64)
 
-    pcm_host = speech_like_batch(args.utts, T, 1000 + rank)
-    pcm = torch.from_numpy(pcm_host.reshape(-1)).to(dev)
-    lens = [T] * args.utts
-    out = torch.empty((L_u * args.utts, cfg.nfilters), dtype=torch.float32, device=dev)
+    if args.workload == "wsj":
+        pcm_host = speech_like_batch(args.utts, T, 1000 + rank).reshape(-1)
+    else:
+        pcm_host = speech_like_batch(1, sum(lens), 1000 + rank).reshape(-1)
+    pcm = torch.from_numpy(pcm_host).to(dev)
+    out = torch.empty((sum(g[1] for g in geo), cfg.nfilters), dtype=torch.float32, device=dev)
     rng = PyRandom(7 + rank)
-    nj = (F_u - 1) * args.utts
+    nj = sum(g[0] - 1 for g in geo)
 
     def step():
         plan.compute(pcm, lens, rng.randbits2(nj), out=out)
@@ -194,7 +211,7 @@ def main():
                           dist if world > 1 else None, dev, before_timed=lambda: plan.set_profiling(True))
     stages, ncalls = plan.stage_times()
 
-    audio_h = world * args.steps * args.utts * T / 16000.0 / 3600.0
+    audio_h = world * args.steps * sum(lens) / 16000.0 / 3600.0
     value = audio_h / elapsed
     # dominant stage: the MFMA autocorrelation (DESIGN.md "Roofline": useful MACs only)
     flops_per_launch = autocorr_flops(plan, support) * frames
@@ -213,8 +230,11 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": "wsj_si284_4s_batches" if args.config == "wsj" else "reverb_et_4s_batches",
-                   "utts_per_step_per_gpu": args.utts, "utt_seconds": args.seconds,
+        "config": {"workload": ("librispeech_960h_scale_u1_30s" if args.workload == "librispeech" else
+                                "wsj_si284_4s_batches" if args.config == "wsj" else "reverb_et_4s_batches"),
+                   "utts_per_step_per_gpu": len(lens),
+                   "utt_seconds": args.seconds if args.workload == "wsj" else "U(1,30), mean %.2f" % (
+                       sum(lens) / 16000.0 / len(lens)),
                    "frames_per_step_per_gpu": frames, "nfilters": cfg.nfilters, "order": cfg.order,
                    "coeff_num": cfg.coeff_num, "fbank": cfg.fbank_type, "support_eps": cfg.support_eps,
                    "autocorr_path": plan.autocorr_path,

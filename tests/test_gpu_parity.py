@@ -269,3 +269,27 @@ def test_reverb_kernel_vs_oracle():
             got = out[off:off + L]
             assert np.abs(got - ref).max() <= 1e-9 * max(1.0, np.abs(ref).max())
             off += T
+
+
+def test_librispeech_scale_lengths_vs_oracle():
+    """BASELINE configs[4] shape: utterances of U(1, 30) s (seeded) plus the 1 s / 30 s extremes, WSJ
+    feature settings, one batch (split over the plan's two-stream sub-batches), against the oracle at
+    TOL: parity at the LibriSpeech-scale length distribution."""
+    from collections import OrderedDict
+    from oracle import fdlp_oracle as O
+    from speech_recognition_tools_amd import FdlpPlan, FeatureConfig, PyRandom
+    import bench
+    rs = np.random.RandomState(960)
+    lens = [int(rs.uniform(1.0, 30.0) * 16000) for _ in range(4)] + [16000, 30 * 16000 - 1]
+    pcm = bench.speech_like_batch(1, sum(lens), 961).reshape(-1)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    sig = OrderedDict(("u%d" % i, pcm[o:o + t]) for i, (o, t) in enumerate(zip(offs, lens)))
+    plan = FdlpPlan(FeatureConfig.wsj(), device=0, max_frames=256)
+    nj = sum(plan.geometry(t)[0] - 1 for t in lens)
+    _, rows, out64 = plan.compute(torch.from_numpy(pcm).cuda(), lens, PyRandom(5).randbits2(nj), want_f64=True)
+    out64 = out64.cpu().numpy()
+    ref = O.compute_utterances(O.FdlpConfig.wsj(), sig, 5)
+    for i, u in enumerate(sig):
+        got = out64[rows[i]:rows[i + 1]]
+        assert got.shape == ref[u].shape, u
+        assert np.abs(got - ref[u]).max() <= TOL, (u, lens[i], np.abs(got - ref[u]).max())
