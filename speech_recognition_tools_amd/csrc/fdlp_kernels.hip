@@ -1298,7 +1298,8 @@ constexpr int autocorr_lds_doubles() {
 }
 
 // -----------------------------------------------------------------------------------------
-// 3v. circular autocorrelation on the fp64 VALU (the default path).
+// 3v. circular autocorrelation on the fp64 VALU (direct path, FDLP_AUTOCORR_VALU=1; MFMA is the default
+//     there: the VALU variant clocks down under full fp64 FMA load, 27.1 vs 25.1 ms per batch).
 //
 // Measured on MI355X: v_fma_f64 sustains 75.8 TFLOP/s, v_mfma_f64_16x16x4f64 only ~51 TFLOP/s
 // (benchmarks/mfma_f64_peak.hip), and the MFMA lag tiling above wastes 13.6 % of its MACs, so a
