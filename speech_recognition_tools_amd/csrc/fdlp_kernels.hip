@@ -1971,6 +1971,54 @@ __global__ __launch_bounds__(256) void ola_log_kernel(DevConsts c, const double*
   if (out) out[o] = decimals >= 0 ? (float)(nearbyint(v * scale10) / scale10) : (float)v;
 }
 
+// Tiled OLA: one workgroup per (utterance, kOlaRows output rows).  The frames overlapping the tile are
+// added in frame order into an LDS tile [row][band] (0 + e_a + e_b, as above), reading each frame's
+// envelope rows [band][t] with consecutive threads on consecutive t (coalesced; the per-thread gather
+// above reads B bands kk doubles apart), then log + floor and row-major stores.
+constexpr int kOlaRows = 32;
+__global__ __launch_bounds__(256) void ola_log_tiled_kernel(DevConsts c, const double* __restrict__ env,
+                                                            const FrameDesc* __restrict__ frames,
+                                                            const UttDesc* __restrict__ utts, float* __restrict__ out,
+                                                            double* __restrict__ out64, int decimals, double scale10) {
+  extern __shared__ double tile[];  // [kOlaRows][B + 1]
+  const int u = blockIdx.y;
+  const UttDesc U = utts[u];
+  const int t0 = blockIdx.x * kOlaRows;
+  if (t0 >= U.L) return;
+  const int nt = min(kOlaRows, U.L - t0);
+  const int B = c.B, BS = c.B + 1, kk = c.kk;
+  const int tid = threadIdx.x;
+  for (int q = tid; q < kOlaRows * BS; q += blockDim.x) tile[q] = 0.0;
+  // frames overlapping [t0, t0 + nt): dst is non-decreasing in k; the last one with dst < t0 + nt,
+  // then down while a frame still reaches t0
+  int lo = 0, hi = U.F - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (frames[U.frame0 + mid].dst < t0 + nt) lo = mid; else hi = mid - 1;
+  }
+  int kf = lo;
+  while (kf > 0 && frames[U.frame0 + kf - 1].dst + kk > t0) --kf;
+  __syncthreads();
+  const int tt = tid % kOlaRows, jj = tid / kOlaRows;  // 8 band lanes x 32 rows
+  for (int k = kf; k <= lo; ++k) {
+    const FrameDesc fd = frames[U.frame0 + k];
+    const int t = t0 + tt;
+    if (t < t0 + nt && t >= fd.dst && t < fd.dst + fd.cnt) {
+      const double* er = env + (int64_t)(U.frame0 + k) * B * kk + fd.src + (t - fd.dst);
+      for (int j = jj; j < B; j += blockDim.x / kOlaRows) tile[tt * BS + j] = tile[tt * BS + j] + er[(int64_t)j * kk];
+    }
+    __syncthreads();
+  }
+  for (int q = tid; q < nt * B; q += blockDim.x) {
+    const int t = q / B, j = q - t * B;
+    const double acc = tile[t * BS + j];
+    const double v = log(acc < 1e-14 ? 1e-14 : acc);  // np.clip(a_min=1e-14) keeps NaN; :227
+    const int64_t o = (U.out_row + t0 + t) * (int64_t)B + j;
+    if (out64) out64[o] = v;
+    if (out) out[o] = decimals >= 0 ? (float)(nearbyint(v * scale10) / scale10) : (float)v;
+  }
+}
+
 // -----------------------------------------------------------------------------------------
 // launch wrappers
 // -----------------------------------------------------------------------------------------
@@ -2274,12 +2322,22 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
 hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc* frames, const UttDesc* utts,
                           int n_utt, int maxL, float* out, double* out_f64, int decimals, hipStream_t s) {
   if (n_utt <= 0 || maxL <= 0) return hipSuccess;
-  const int64_t per = (int64_t)maxL * c.B;
-  dim3 grid((unsigned)((per + 255) / 256), n_utt);
   double scale10 = 1.0;
   for (int i = 0; i < decimals; ++i) scale10 *= 10.0;
-  hipLaunchKernelGGL(ola_log_kernel, grid, dim3(256), 0, s, c, env, frames, utts, out, out_f64, decimals,
-                     scale10);
+  static const bool gather = getenv("FDLP_OLA_GATHER") != nullptr;
+  if (gather) {
+    const int64_t per = (int64_t)maxL * c.B;
+    dim3 grid((unsigned)((per + 255) / 256), n_utt);
+    hipLaunchKernelGGL(ola_log_kernel, grid, dim3(256), 0, s, c, env, frames, utts, out, out_f64, decimals,
+                       scale10);
+  } else {
+    dim3 grid((unsigned)((maxL + kOlaRows - 1) / kOlaRows), n_utt);
+    const size_t lds = sizeof(double) * kOlaRows * (size_t)(c.B + 1);
+    if (lds > 65536)
+      (void)hipFuncSetAttribute((const void*)ola_log_tiled_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(ola_log_tiled_kernel, grid, dim3(256), lds, s, c, env, frames, utts, out, out_f64, decimals,
+                       scale10);
+  }
   return hipGetLastError();
 }
 
