@@ -1,20 +1,24 @@
 #!/usr/bin/env bash
-# Round evidence on one GPU box: full bench (with CPU baseline), rocprofv3 kernel-trace stats and
-# separate PMC passes (FETCH_SIZE / WRITE_SIZE / clocks+MFMA busy) of the same bench command.
+# Round evidence on one GPU box: rocprofv3 kernel-trace stats and separate PMC passes (FETCH_SIZE /
+# WRITE_SIZE / clocks+MFMA busy / VALU / LDS) of the same bench command, then the full bench (with CPU
+# baseline), which reads its roofline traffic from the PMC summary written here first.
 # Outputs under gpurun_out/evidence/; copy what is judged into profiles/ (see DESIGN.md).
+# TAG (default r01x) names that summary: profiles/${TAG}_pmc.json (box-local copy for the bench).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/evidence
+TAG=${TAG:-r01x}
 mkdir -p $O
 BARGS=${BENCH_ARGS:-"--steps 5 --warmup 1 --no-cpu-baseline"}
-timeout -k 10 600 python3 bench.py > $O/bench_full.log 2>&1 || { echo "bench failed"; tail -20 $O/bench_full.log; exit 2; }
-tail -1 $O/bench_full.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3 bench.py $BARGS > $O/trace.log 2>&1 || { echo "trace failed"; tail -20 $O/trace.log; exit 3; }
+python3 scripts/rocpd_summary.py $O/trace/run_results.db $O/kernel_trace_stats.csv > /dev/null || true
 i=0
 for pmc in FETCH_SIZE WRITE_SIZE "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU" "SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS"; do
   i=$((i+1))
   timeout -k 10 600 rocprofv3 --kernel-trace --pmc $pmc -d $O/pmc_$i -o run -- python3 bench.py $BARGS > $O/pmc_$i.log 2>&1 || { echo "pmc $pmc failed"; tail -20 $O/pmc_$i.log; exit 4; }
 done
 python3 scripts/pmc_report.py "$O/pmc_*/*.db" $O/pmc.json > $O/pmc.txt 2>&1 || true
-find $O -name "*.db" | head -20
+cp $O/pmc.json profiles/${TAG}_pmc.json
+timeout -k 10 600 python3 bench.py > $O/bench_full.log 2>&1 || { echo "bench failed"; tail -20 $O/bench_full.log; exit 2; }
+tail -1 $O/bench_full.log
