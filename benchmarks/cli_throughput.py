@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=4.0)
     ap.add_argument("--workers", type=int, nargs="+", default=[1, 4, 8])
     ap.add_argument("--batch-frames", type=int, default=8192)
+    ap.add_argument("--profile", default=None, help="write cProfile stats of the last run to this file")
     a = ap.parse_args()
     from bench import speech_like_batch
     from speech_recognition_tools_amd.featgen.computeFDLPSpectrogram import build_parser, getFeats
@@ -51,10 +52,21 @@ def main():
             args = build_parser().parse_args([os.path.join(d, "wav.scp"), os.path.join(d, "o%d" % w),
                                               "--io_workers=%d" % w] + opts)
             sys.stdout = devnull
+            prof = None
+            if a.profile:
+                import cProfile
+                prof = cProfile.Profile()
+                prof.enable()
             t0 = time.perf_counter()
             getFeats(args, return_feats=False)
             el = time.perf_counter() - t0
             sys.stdout = so
+            if prof is not None:
+                import pstats
+                prof.disable()
+                with open(a.profile, "w") as fh:
+                    pstats.Stats(prof, stream=fh).sort_stats("cumulative").print_stats(40)
+                    pstats.Stats(prof, stream=fh).sort_stats("tottime").print_stats(30)
             audio_h = a.utts * T / 16000.0 / 3600.0
             print(json.dumps({"metric": "compute-fdlp-feats end-to-end audio-hours/s (WAV in, ark out)",
                               "value": audio_h / el, "unit": "audio-hours/s", "io_workers": w,

@@ -148,6 +148,7 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
         nonlocal pending, pending_frames
         if not pending:
             return
+        sys.stdout.flush()
         lens = [x[1].shape[0] for x in pending]
         pcm_host = torch.from_numpy(np.concatenate([x[1] for x in pending])).pin_memory()
         pcm = pcm_host.to(torch.device("cuda", device), non_blocking=True)
@@ -197,8 +198,9 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
             off, alpha = 0, 0.0
             if noise is not None:                                           # :166
                 off, alpha = add_noise_to_wav_params(sig, noise, snr, noise_rng.rand())
+            # the reference's progress line; flushed once per device batch (flush()) rather than per
+            # utterance, which cost ~20 us per line on 4 s utterances
             print('%s: Computing Features for file: %s' % (sys.argv[0], uttid))
-            sys.stdout.flush()
             if pending_frames + F > plan.max_frames:
                 flush()
             if F > plan.max_frames:
