@@ -158,6 +158,11 @@ int fdlp_autocorr_path(const fdlp_plan* plan);
 /* Lower-skirt / flat-top / upper-skirt split of every band, [0,m1) [m1,m2) [m2,N), used by the
  * STRUCTURED path; FDLP_E_INVALID when the filterbank does not have it. */
 int fdlp_plan_regions(const fdlp_plan* plan, int32_t* m1, int32_t* m2);
+/* The flat-top sweep of FDLP_AC_STRUCTURED (DESIGN.md "Lag-parallel VALU sweeps"): number of chains
+ * (0 when the VALU sweeps are not available), position parts, and for up to cap events (S, band, type
+ * 0 restart / 1 emit, chain) in sweep order; *nev receives the event count. */
+int fdlp_plan_flat_events(const fdlp_plan* plan, int32_t* chains, int32_t* parts, int32_t* nev, int32_t* events,
+                          int32_t cap);
 /* fdlp_compute splits a batch of F frames into min(n_sub, F/256) sub-batches that alternate
  * between the caller's stream and a second stream of the plan, so the MFMA-bound autocorrelation
  * of one sub-batch can overlap the VALU-bound kernels of the other (default 1 = serial: on MI355X

@@ -921,6 +921,22 @@ int fdlp_set_autocorr_path(fdlp_plan* p, int32_t path) {
   return FDLP_OK;
 }
 
+int fdlp_plan_flat_events(const fdlp_plan* p, int32_t* chains, int32_t* parts, int32_t* nev, int32_t* events,
+                          int32_t cap) {
+  if (!p) return fail(FDLP_E_INVALID, "fdlp_plan_flat_events: null plan");
+  const bool ok = p->sk_avail && p->vs_avail;
+  if (chains) *chains = ok ? p->sk.fl_C : 0;
+  if (parts) *parts = ok ? p->sk.fl_H : 0;
+  const int n = ok ? (int)p->sk.fl.size() : 0;
+  if (nev) *nev = n;
+  if (events)
+    for (int k = 0; k < n && k < cap; ++k) {
+      const fdlp::FlatEv& e = p->sk.fl[k];
+      events[4 * k] = e.S; events[4 * k + 1] = e.band; events[4 * k + 2] = e.type; events[4 * k + 3] = e.chain;
+    }
+  return FDLP_OK;
+}
+
 int fdlp_plan_regions(const fdlp_plan* p, int32_t* m1, int32_t* m2) {
   if (!p) return fail(FDLP_E_INVALID, "fdlp_plan_regions: null plan");
   if (!p->sk_avail) return fail(FDLP_E_INVALID, "filterbank has no skirt/flat-top split (structured path unavailable)");

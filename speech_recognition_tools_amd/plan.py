@@ -257,6 +257,15 @@ class FdlpPlan:
         check(lib.fdlp_plan_regions(self._h, ptr(m1, ctypes.c_int32), ptr(m2, ctypes.c_int32)))
         return m1, m2
 
+    def flat_events(self):
+        """(chains, parts, events[n, 4] = (S, band, type, chain)) of the flat-top sweep, sweep order;
+        chains == 0 when the lag-parallel VALU sweeps are not available for this plan."""
+        C, H, n = _lib.c_i32(), _lib.c_i32(), _lib.c_i32()
+        check(lib.fdlp_plan_flat_events(self._h, ctypes.byref(C), ctypes.byref(H), ctypes.byref(n), None, 0))
+        ev = np.zeros((n.value, 4), dtype=np.int32)
+        check(lib.fdlp_plan_flat_events(self._h, None, None, ctypes.byref(n), ptr(ev, ctypes.c_int32), n.value))
+        return C.value, H.value, ev
+
     def set_pipeline(self, n_sub: int):
         check(lib.fdlp_set_pipeline(self._h, int(n_sub)))
 
