@@ -1694,7 +1694,11 @@ __device__ __forceinline__ void lattice_durbin(double (&A)[SL], double (&B)[SL],
 // lpc_env with the lattice Durbin: persistent waves (grid-stride over groups of 4 items), r read
 // straight into registers, LDS only for a (cepstrum) and c (envelope).  Same outputs as lpc_env_kernel.
 constexpr int kEnvChunk = 5;  // envelope slots held in registers at a time
-template <int SL>
+// CB > 0 (M <= 16 CB): the cepstrum's finished blocks take c_k from the registers of the lane that
+// computed it (v_fmac_f64_dpp row_newbcast, the broadcast is the FMA's source modifier) instead of an
+// LDS read per term: one LDS read (alpha_{n-k}) and one FMA per term instead of two reads, a multiply
+// and an FMA.  CB = 0: the LDS form for any M.
+template <int SL, int CB = 0>
 __global__ __launch_bounds__(64, 4) void lpc_env_lattice_kernel(LpcEnvArgs A_) {
   extern __shared__ double sh[];
   const LpcEnvArgs& A = A_;
@@ -1753,7 +1757,48 @@ __global__ __launch_bounds__(64, 4) void lpc_env_lattice_kernel(LpcEnvArgs A_) {
     if (valid && A.a_out && lane0) A.gg_out[item] = gg;
     wave_lds_sync();
     // ---- phase 2: cepstrum (features.py:233-246), as in lpc_env_kernel -------------------------
-    for (int b0 = 0; b0 < ((FDLP_LPC_PHASES & 2) ? M : 0); b0 += 16) {
+    if constexpr (CB > 0) {
+      double kc[CB];  // lane l: n c_n for n = 16 b + l of every finished block b (0 for n = 0)
+#pragma unroll
+      for (int b = 0; b < CB; ++b) {
+        const int b0 = 16 * b;
+        if (b0 >= ((FDLP_LPC_PHASES & 2) ? M : 0)) break;
+        const int n = b0 + l;
+        const double inv_n = 1.0 / (double)(n > 0 ? n : 1);
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        if (b > 0) asm volatile("s_nop 1");  // kc[b - 1] was just written: DPP reads need 2 wait states
+#pragma unroll
+        for (int bp = 0; bp < b; ++bp) {
+          const double* al = la + n - 16 * bp;  // alpha_{n - k} = la[n - k], k = 16 bp + j
+          fmac_bcast<0>(a0, kc[bp], al[0]);
+          fmac_bcast<1>(a1, kc[bp], al[-1]);
+          fmac_bcast<2>(a2, kc[bp], al[-2]);
+          fmac_bcast<3>(a3, kc[bp], al[-3]);
+          fmac_bcast<4>(a0, kc[bp], al[-4]);
+          fmac_bcast<5>(a1, kc[bp], al[-5]);
+          fmac_bcast<6>(a2, kc[bp], al[-6]);
+          fmac_bcast<7>(a3, kc[bp], al[-7]);
+          fmac_bcast<8>(a0, kc[bp], al[-8]);
+          fmac_bcast<9>(a1, kc[bp], al[-9]);
+          fmac_bcast<10>(a2, kc[bp], al[-10]);
+          fmac_bcast<11>(a3, kc[bp], al[-11]);
+          fmac_bcast<12>(a0, kc[bp], al[-12]);
+          fmac_bcast<13>(a1, kc[bp], al[-13]);
+          fmac_bcast<14>(a2, kc[bp], al[-14]);
+          fmac_bcast<15>(a3, kc[bp], al[-15]);
+        }
+        double acc = (a0 + a1) + (a2 + a3);
+        double mine = 0.0;
+        cep_block_step<0>(b0, M, l, gg, inv_n, la, n, acc, mine);
+        kc[b] = n == 0 ? 0.0 : (double)n * mine;
+        if (n < M) {
+          cs[n] = mine;
+          if (valid && A.cep_out) A.cep_out[(int64_t)item * M + n] = mine;
+        }
+      }
+      wave_lds_sync();
+    }
+    for (int b0 = 0; b0 < ((CB == 0 && (FDLP_LPC_PHASES & 2)) ? M : 0); b0 += 16) {
       const int n = b0 + l;
       const double inv_n = 1.0 / (double)(n > 0 ? n : 1);
       // finished blocks: four independent FMA chains (the trip count is uniform across the wave)
@@ -2264,25 +2309,25 @@ int lpc_env_region(int p, int M) {
   return (need + 15) / 32 * 32 + 16;  // = 16 mod 32 doubles: the 4 items of a wave hit disjoint bank halves
 }
 
-template <int SL>
+template <int SL, int CB = 0>
 static hipError_t launch_lpc_lattice_sl(const LpcEnvArgs& A, size_t lds, hipStream_t s) {
   static int per_cu = -1, cus = 0;  // resident waves per CU at this LDS size (one wave per block)
   static size_t per_cu_lds = 0;
   if (per_cu < 0 || per_cu_lds != lds) {
     if (lds > 65536)
-      (void)hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL>,
+      (void)hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL, CB>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     int dev = 0, n = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lpc_env_lattice_kernel<SL>, 64, lds) != hipSuccess || n < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lpc_env_lattice_kernel<SL, CB>, 64, lds) != hipSuccess || n < 1)
       n = 4;
     per_cu = n;
     per_cu_lds = lds;
   }
   const int groups = (A.items + 3) / 4;
   const int grid = std::min(groups, std::max(1, per_cu * std::max(cus, 1)));
-  hipLaunchKernelGGL((lpc_env_lattice_kernel<SL>), dim3(grid), dim3(64), lds, s, A);
+  hipLaunchKernelGGL((lpc_env_lattice_kernel<SL, CB>), dim3(grid), dim3(64), lds, s, A);
   return hipGetLastError();
 }
 
@@ -2299,6 +2344,15 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
     const int NAL = (c.M > c.p + 1 ? c.M : c.p + 1) + 16;
     A.region = (NAL + c.M + 15) / 32 * 32 + 16;  // = 16 mod 32 doubles (disjoint bank halves per item)
     const size_t lds = sizeof(double) * (4 * (size_t)A.region);
+    static const bool lds_cep = getenv("FDLP_CEP_LDS") != nullptr;
+    if (!lds_cep && c.M <= 16 * 7 && SL >= 9 && SL <= 11) {  // register-broadcast cepstrum (recipes: p 150, M 100)
+      switch (SL) {
+        case 9: return launch_lpc_lattice_sl<9, 7>(A, lds, s);
+        case 10: return launch_lpc_lattice_sl<10, 7>(A, lds, s);
+        case 11: return launch_lpc_lattice_sl<11, 7>(A, lds, s);
+        default: break;
+      }
+    }
     switch (SL) {
 #define FDLP_SL_CASE(n) case n: return launch_lpc_lattice_sl<n>(A, lds, s);
       FDLP_SL_CASE(1) FDLP_SL_CASE(2) FDLP_SL_CASE(3) FDLP_SL_CASE(4) FDLP_SL_CASE(5) FDLP_SL_CASE(6)
