@@ -145,7 +145,7 @@ int fdlp_set_debug(fdlp_plan* plan, int32_t keep_intermediates);
  * filterbank with a fixed slope (fbank_type cochlear,..,fixed=1,..; DESIGN.md "Structured
  * autocorrelation"), its three sweeps (lower skirt, flat tops, upper skirt) lag-parallel on the fp64
  * VALU; FDLP_AC_STRUCTURED_MFMA: the same algorithm with MFMA lag-tile skirt sweeps and per-band
- * flat tops (also used when the VALU sweeps do not fit: more than 256 lags or 8 overlapping flat
+ * flat tops (also used when the VALU sweeps do not fit: more than 160 lags or 8 overlapping flat
  * tops).  FDLP_AC_AUTO (plan default) picks the first available of STRUCTURED, STRUCTURED_MFMA,
  * DIRECT.  fdlp_set_autocorr_path returns FDLP_E_INVALID when the structured paths are not
  * available; fdlp_autocorr_path returns the path in use or a negative error code. */

@@ -2172,8 +2172,10 @@ hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* 
 }
 
 int vsweep_lanes_lags(int nlags) {
+  // up to 160 lags (p <= 158): with more lags per lane the chains and the window no longer fit the
+  // registers of two waves per SIMD (spills), and such plans keep the MFMA sweeps
   const int a = (nlags + 15) / 16;
-  for (int v : {4, 8, 10, 12, 16})
+  for (int v : {4, 8, 10})
     if (a <= v) return v;
   return 0;
 }
@@ -2210,8 +2212,6 @@ static hipError_t launch_vsweep(const DevConsts& c, const double* dct, int nfram
     case 4: return launch_vsweep_a<4>(c, dct, nframes, r, rup, rflat, rpart, s);
     case 8: return launch_vsweep_a<8>(c, dct, nframes, r, rup, rflat, rpart, s);
     case 10: return launch_vsweep_a<10>(c, dct, nframes, r, rup, rflat, rpart, s);
-    case 12: return launch_vsweep_a<12>(c, dct, nframes, r, rup, rflat, rpart, s);
-    case 16: return launch_vsweep_a<16>(c, dct, nframes, r, rup, rflat, rpart, s);
     default: return hipErrorInvalidValue;
   }
 }
