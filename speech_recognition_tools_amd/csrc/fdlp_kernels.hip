@@ -1668,15 +1668,20 @@ __device__ __forceinline__ void lattice_phase(double (&A)[SL], double (&B)[SL], 
     rE = fma(rE, fma(-E, rE, 1.0), rE);
     rE = fma(rE, fma(-E, rE, 1.0), rE);
     const double kappa = -acc * rE;
-    double rot[Q + 1];
+    // zB without a select: lanes 1..15 take lane l-1 (row_shr:1); lane 0 takes 0 (slot 0, bound_ctrl)
+    // or keeps the old value, a 64-bit row_newbcast:15 of the previous slot (one v_mov_b64_dpp)
+    double bsh[Q + 1];
+    bsh[0] = __builtin_amdgcn_update_dpp(0.0, B[0], 0x111, 0xF, 0xF, true);
 #pragma unroll
-    for (int s = 0; s <= Q; ++s) rot[s] = dpp_f64<0x121>(B[s]);  // row_ror:1
+    for (int s = 1; s <= Q; ++s) {
+      const double prev15 = __builtin_amdgcn_update_dpp(0.0, B[s - 1], 0x15F, 0xF, 0xF, true);
+      bsh[s] = __builtin_amdgcn_update_dpp(prev15, B[s], 0x111, 0xF, 0xF, false);
+    }
 #pragma unroll
     for (int s = 0; s <= Q; ++s) {
-      // B first: its old value lives on in rot[], so both updates are in place (no register copies)
-      const double bsh = lane0 ? (s == 0 ? 0.0 : rot[s - 1]) : rot[s];
-      B[s] = fma(kappa, A[s], bsh);
-      A[s] = fma(kappa, bsh, A[s]);
+      // B first: its old value lives on in bsh[], so both updates are in place (no register copies)
+      B[s] = fma(kappa, A[s], bsh[s]);
+      A[s] = fma(kappa, bsh[s], A[s]);
     }
     E = E * (1.0 - kappa * kappa);
   }
