@@ -60,7 +60,7 @@ def build_parser():
     parser.add_argument('--support_eps', type=float, default=None,
                         help='filter taps below eps*peak are skipped in the autocorrelation (0 = exact)')
     parser.add_argument('--io_workers', type=int, default=4,
-                        help='threads reading/parsing the scp entries ahead of the device (1 = inline)')
+                        help='threads reading `<cmd> |` scp entries ahead of the device (plain files are read inline)')
     parser.add_argument('--cmvn_stats', type=str, default=None,
                         help='also write the global CMVN stats of the written features (Kaldi compute-cmvn-stats '
                              'format, accumulated on the device) to this file')

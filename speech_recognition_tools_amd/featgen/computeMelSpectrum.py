@@ -40,7 +40,7 @@ def get_args(argv=None):
     parser.add_argument('--noise_seed', type=int, default=None, help='seed of the noise offsets (np.random.seed)')
     parser.add_argument('--device', type=int, default=None, help='HIP device (default: LOCAL_RANK or 0)')
     parser.add_argument('--batch_frames', type=int, default=65536, help='frames per GPU batch')
-    parser.add_argument('--io_workers', type=int, default=4, help='threads reading the scp entries ahead')
+    parser.add_argument('--io_workers', type=int, default=4, help='threads reading `<cmd> |` scp entries ahead (plain files are read inline)')
     parser.add_argument('--ark_precision', type=int, default=3, help="decimals of the text ark ('%%.3f')")
     return parser.parse_args(argv)
 

@@ -47,7 +47,7 @@ def get_args(argv=None):
     # MI355X additions (all optional)
     parser.add_argument('--device', type=int, default=None, help='HIP device (default: LOCAL_RANK or 0)')
     parser.add_argument('--batch_frames', type=int, default=8192, help='analysis frames per GPU batch')
-    parser.add_argument('--io_workers', type=int, default=4, help='threads reading the scp entries ahead')
+    parser.add_argument('--io_workers', type=int, default=4, help='threads reading `<cmd> |` scp entries ahead (plain files are read inline)')
     parser.add_argument('--ark_precision', type=int, default=3, help="decimals of the text ark ('%%.3f')")
     return parser.parse_args(argv)
 
