@@ -1704,7 +1704,10 @@ constexpr int kEnvChunk = 5;  // envelope slots held in registers at a time
 // LDS read per term: one LDS read (alpha_{n-k}) and one FMA per term instead of two reads, a multiply
 // and an FMA.  CB = 0: the LDS form for any M.
 template <int SL, int CB = 0>
-__global__ __launch_bounds__(64, 4) void lpc_env_lattice_kernel(LpcEnvArgs A_) {
+#ifndef FDLP_LAT_WAVES
+#define FDLP_LAT_WAVES 4  // waves per SIMD the lattice kernel is compiled for (register budget)
+#endif
+__global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(LpcEnvArgs A_) {
   extern __shared__ double sh[];
   const LpcEnvArgs& A = A_;
   const int ngroups = (A.items + 3) >> 2;
