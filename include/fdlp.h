@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define FDLP_ABI_VERSION 2
+#define FDLP_ABI_VERSION 3
 
 enum {
   FDLP_OK = 0,
@@ -173,6 +173,9 @@ int fdlp_set_pipeline(fdlp_plan* plan, int32_t n_sub);
  * cep [F,B,coeff_num]; env [F,B,kk]. */
 int fdlp_debug_fetch(fdlp_plan* plan, int32_t n_frames, double* dct, double* r, double* a,
                      double* gg, double* cep, double* env);
+/* Same for the frames [first_frame, first_frame + n_frames) of the most recent batch (ABI 3). */
+int fdlp_debug_fetch_range(fdlp_plan* plan, int32_t first_frame, int32_t n_frames, double* dct, double* r,
+                           double* a, double* gg, double* cep, double* env);
 
 /* Per-stage device time (HIP events on the stream each stage runs on) of every fdlp_compute since
  * profiling was (re)enabled.  Stages: 0 frames+column DFT, 1 row DFT+DCT, 2 autocorrelation,

@@ -98,6 +98,7 @@ SIGNATURES = {
     "fdlp_ola_table": (c_i32, [c_p, c_i64, P_u8, P_i32, P_i32, P_i32]),
     "fdlp_compute": (c_i32, [c_p, ctypes.POINTER(FdlpBatchC), c_p]),
     "fdlp_debug_fetch": (c_i32, [c_p, c_i32, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl]),
+    "fdlp_debug_fetch_range": (c_i32, [c_p, c_i32, c_i32, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl]),
     "fdlp_set_profiling": (c_i32, [c_p, c_i32]),
     "fdlp_set_debug": (c_i32, [c_p, c_i32]),
     "fdlp_set_autocorr_path": (c_i32, [c_p, c_i32]),
@@ -149,7 +150,7 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.fdlp_abi_version() != 2:
+    if lib.fdlp_abi_version() != 3:
         raise ImportError("libfdlp_hip.so ABI mismatch")
     return lib
 

@@ -82,6 +82,10 @@ struct DevConsts {
   int fl_H = 1;
   int fl_part_lo[kMaxFlatParts] = {0}, fl_part_hi[kMaxFlatParts] = {0}, fl_part_ev[kMaxFlatParts + 1] = {0};
   const int2* fl_band = nullptr;  // [B] (chain, bitmask of the parts h < fl_H - 1 it needs a partial from)
+  // persistent LPC kernel: resident blocks on the plan's device (prepare_lpc_env, at plan creation)
+  int lpc_blocks = 0;
+  int lpc_lds_durbin = 0;  // FDLP_LPC_LDS at plan creation: the LDS Durbin instead of the lattice
+  int lpc_cep_lds = 0;     // FDLP_CEP_LDS at plan creation: the LDS cepstrum form for every M
 };
 
 }  // namespace fdlp
@@ -117,6 +121,9 @@ hipError_t launch_cepstrum(int p, int M, const double* a, const double* gg, int 
 hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int items, double* env,
                           double* a_out, double* gg_out, double* cep_out, hipStream_t s);
 int lpc_env_region(int p, int M);
+// Per-plan launch setup of launch_lpc_env for the current device: sets the kernel's large-LDS
+// attribute and stores the resident block count in c.lpc_blocks.
+hipError_t prepare_lpc_env(DevConsts& c);
 int autocorr_tiles(int nlags);
 int band_fused_fits(int nlags, int p, int M, int kk);
 hipError_t launch_band_fused(const DevConsts& c, int odd_zero, const double* dct, int items, double* r_dbg,

@@ -23,6 +23,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -2317,26 +2318,60 @@ int lpc_env_region(int p, int M) {
   return (need + 15) / 32 * 32 + 16;  // = 16 mod 32 doubles: the 4 items of a wave hit disjoint bank halves
 }
 
-template <int SL, int CB = 0>
-static hipError_t launch_lpc_lattice_sl(const LpcEnvArgs& A, size_t lds, hipStream_t s) {
-  static int per_cu = -1, cus = 0;  // resident waves per CU at this LDS size (one wave per block)
-  static size_t per_cu_lds = 0;
-  if (per_cu < 0 || per_cu_lds != lds) {
-    if (lds > 65536)
-      (void)hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL, CB>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lpc_env_lattice_kernel<SL, CB>, 64, lds) != hipSuccess || n < 1)
-      n = 4;
-    per_cu = n;
-    per_cu_lds = lds;
+// Lattice-kernel instantiation of a plan: calls fn(integral_constant<SL>, integral_constant<CB>) or
+// returns hipErrorNotSupported when the plan runs the LDS Durbin (lpc_env_kernel).
+template <class Fn>
+static hipError_t lattice_dispatch(const DevConsts& c, Fn&& fn) {
+  using std::integral_constant;
+  const int SL = (c.p + 1 + 15) / 16;
+  if (SL > 16 || c.lpc_lds_durbin) return hipErrorNotSupported;
+  if (!c.lpc_cep_lds && c.M <= 16 * 7 && SL >= 9 && SL <= 11) {  // register-broadcast cepstrum (recipes: p 150, M 100)
+    switch (SL) {
+      case 9: return fn(integral_constant<int, 9>{}, integral_constant<int, 7>{});
+      case 10: return fn(integral_constant<int, 10>{}, integral_constant<int, 7>{});
+      case 11: return fn(integral_constant<int, 11>{}, integral_constant<int, 7>{});
+      default: break;
+    }
   }
-  const int groups = (A.items + 3) / 4;
-  const int grid = std::min(groups, std::max(1, per_cu * std::max(cus, 1)));
-  hipLaunchKernelGGL((lpc_env_lattice_kernel<SL, CB>), dim3(grid), dim3(64), lds, s, A);
-  return hipGetLastError();
+  switch (SL) {
+#define FDLP_SL_CASE(n) case n: return fn(integral_constant<int, n>{}, integral_constant<int, 0>{});
+    FDLP_SL_CASE(1) FDLP_SL_CASE(2) FDLP_SL_CASE(3) FDLP_SL_CASE(4) FDLP_SL_CASE(5) FDLP_SL_CASE(6)
+    FDLP_SL_CASE(7) FDLP_SL_CASE(8) FDLP_SL_CASE(9) FDLP_SL_CASE(10) FDLP_SL_CASE(11) FDLP_SL_CASE(12)
+    FDLP_SL_CASE(13) FDLP_SL_CASE(14) FDLP_SL_CASE(15) FDLP_SL_CASE(16)
+#undef FDLP_SL_CASE
+    default: return hipErrorNotSupported;
+  }
+}
+
+static size_t lattice_lds(const DevConsts& c) {
+  const int NAL = (c.M > c.p + 1 ? c.M : c.p + 1) + 16;
+  const int region = (NAL + c.M + 15) / 32 * 32 + 16;  // = 16 mod 32 doubles (disjoint bank halves per item)
+  return sizeof(double) * 4 * (size_t)region;
+}
+
+hipError_t prepare_lpc_env(DevConsts& c) {
+  c.lpc_lds_durbin = getenv("FDLP_LPC_LDS") != nullptr;
+  c.lpc_cep_lds = getenv("FDLP_CEP_LDS") != nullptr;
+  c.lpc_blocks = 0;
+  int dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  const size_t lds = lattice_lds(c);
+  int per_cu = 0;
+  e = lattice_dispatch(c, [&](auto sl, auto cb) -> hipError_t {
+    constexpr int SL = decltype(sl)::value, CB = decltype(cb)::value;
+    if (lds > 65536) {
+      const hipError_t a = hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL, CB>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (a != hipSuccess) return a;
+    }
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lpc_env_lattice_kernel<SL, CB>, 64, lds);
+  });
+  if (e == hipErrorNotSupported) return hipSuccess;  // LDS Durbin: one block per item group, no setup
+  if (e != hipSuccess) return e;
+  c.lpc_blocks = std::max(1, per_cu) * std::max(1, cus);
+  return hipSuccess;
 }
 
 hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int items, double* env,
@@ -2347,28 +2382,15 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
   A.odd_zero = odd_zero; A.items = items; A.region = lpc_env_region(c.p, c.M);
   A.r = r; A.weights = c.weights; A.env_cos = c.env_cos; A.env_win = c.env_win; A.env = env;
   A.a_out = a_out; A.gg_out = gg_out; A.cep_out = cep_out;
-  const int SL = (c.p + 1 + 15) / 16;
-  if (SL <= 16 && !getenv("FDLP_LPC_LDS")) {  // lattice Durbin in registers
-    const int NAL = (c.M > c.p + 1 ? c.M : c.p + 1) + 16;
-    A.region = (NAL + c.M + 15) / 32 * 32 + 16;  // = 16 mod 32 doubles (disjoint bank halves per item)
-    const size_t lds = sizeof(double) * (4 * (size_t)A.region);
-    static const bool lds_cep = getenv("FDLP_CEP_LDS") != nullptr;
-    if (!lds_cep && c.M <= 16 * 7 && SL >= 9 && SL <= 11) {  // register-broadcast cepstrum (recipes: p 150, M 100)
-      switch (SL) {
-        case 9: return launch_lpc_lattice_sl<9, 7>(A, lds, s);
-        case 10: return launch_lpc_lattice_sl<10, 7>(A, lds, s);
-        case 11: return launch_lpc_lattice_sl<11, 7>(A, lds, s);
-        default: break;
-      }
-    }
-    switch (SL) {
-#define FDLP_SL_CASE(n) case n: return launch_lpc_lattice_sl<n>(A, lds, s);
-      FDLP_SL_CASE(1) FDLP_SL_CASE(2) FDLP_SL_CASE(3) FDLP_SL_CASE(4) FDLP_SL_CASE(5) FDLP_SL_CASE(6)
-      FDLP_SL_CASE(7) FDLP_SL_CASE(8) FDLP_SL_CASE(9) FDLP_SL_CASE(10) FDLP_SL_CASE(11) FDLP_SL_CASE(12)
-      FDLP_SL_CASE(13) FDLP_SL_CASE(14) FDLP_SL_CASE(15) FDLP_SL_CASE(16)
-#undef FDLP_SL_CASE
-      default: break;
-    }
+  if (c.lpc_blocks > 0) {  // lattice Durbin in registers, persistent grid (prepare_lpc_env)
+    const size_t lds = lattice_lds(c);
+    A.region = (int)(lds / (4 * sizeof(double)));
+    const int grid = std::min((items + 3) / 4, c.lpc_blocks);
+    return lattice_dispatch(c, [&](auto sl, auto cb) -> hipError_t {
+      constexpr int SL = decltype(sl)::value, CB = decltype(cb)::value;
+      hipLaunchKernelGGL((lpc_env_lattice_kernel<SL, CB>), dim3(grid), dim3(64), lds, s, A);
+      return hipGetLastError();
+    });
   }
   const size_t lds = sizeof(double) * (4 * (size_t)A.region);
   switch ((c.env_nfft / 4 + 1 + 15) / 16) {  // envelope slots: u = 0 .. env_nfft/4

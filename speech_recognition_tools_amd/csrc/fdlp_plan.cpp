@@ -34,6 +34,28 @@ using fdlp::fail;
 
 namespace {
 
+// Makes `dev` current for the scope of an ABI call and restores the caller's device afterwards.
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(int dev) {
+    if (dev < 0) return;
+    if ((err_ = hipGetDevice(&prev_)) != hipSuccess) return;
+    if (prev_ != dev) {
+      err_ = hipSetDevice(dev);
+      switched_ = err_ == hipSuccess;
+    }
+  }
+  ~DeviceGuard() {
+    if (switched_) (void)hipSetDevice(prev_);
+  }
+  hipError_t status() const { return err_; }
+
+ private:
+  int prev_ = -1;
+  bool switched_ = false;
+  hipError_t err_ = hipSuccess;
+};
+
 // numpy.linspace(start, stop, num): i*step + start, last element = stop exactly.
 std::vector<double> linspace(double start, double stop, int num) {
   std::vector<double> y(num);
@@ -620,7 +642,8 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) PLAN_FAIL(FDLP_E_HIP, "no HIP device visible");
   if (device < 0 || device >= ndev) PLAN_FAIL(FDLP_E_INVALID, "device index out of range");
-  if (hipSetDevice(device) != hipSuccess) PLAN_FAIL(FDLP_E_HIP, "hipSetDevice failed");
+  DeviceGuard dg(device);  // restored when plan creation returns
+  if (dg.status() != hipSuccess) PLAN_FAIL(FDLP_E_HIP, "hipSetDevice failed");
   PLAN_TRY(upload(&p->d_fbank, dense.data(), dense.size()));
   PLAN_TRY(upload(&p->d_lo, p->lo.data(), p->lo.size()));
   PLAN_TRY(upload(&p->d_hi, p->hi.data(), p->hi.size()));
@@ -661,6 +684,9 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
       for (int h = 0; h <= fdlp::kMaxFlatParts; ++h) d.fl_part_ev[h] = p->sk.part_ev[h];
     }
   }
+
+  // launch geometry of the persistent LPC kernel for this device (occupancy, large-LDS attribute)
+  if (fdlp::prepare_lpc_env(d) != hipSuccess) PLAN_FAIL(FDLP_E_HIP, "LPC kernel launch setup failed");
 
   // workspace
   const size_t F = (size_t)c.max_frames, items = F * p->B;
@@ -772,8 +798,8 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
   if (!b->out_dev && !b->out_f64_dev) return fail(FDLP_E_INVALID, "fdlp_compute: no output buffer");
   if (p->device < 0) return fail(FDLP_E_INVALID, "fdlp_compute: host-only plan (created with device < 0)");
   hipStream_t s = (hipStream_t)stream;
-  int cur = -1;
-  if (hipGetDevice(&cur) == hipSuccess && cur != p->device) HIP_TRY(hipSetDevice(p->device));
+  DeviceGuard dg(p->device);  // the caller's current device is restored on return
+  HIP_TRY(dg.status());
   // staging buffers may still feed the previous call's copies
   if (p->staging_pending) {
     HIP_TRY(hipEventSynchronize(p->staging_done));
@@ -983,18 +1009,26 @@ int fdlp_stage_times(fdlp_plan* p, double* ms_sum, int32_t* n_calls) {
   return FDLP_OK;
 }
 
+int fdlp_debug_fetch_range(fdlp_plan* p, int32_t f0, int32_t n, double* dct, double* r, double* a, double* gg,
+                           double* cep, double* env) {
+  if (!p || f0 < 0 || n < 0 || (int64_t)f0 + n > p->max_frames || p->device < 0)
+    return fail(FDLP_E_INVALID, "fdlp_debug_fetch: bad args");
+  DeviceGuard dg(p->device);
+  HIP_TRY(dg.status());
+  HIP_TRY(hipDeviceSynchronize());
+  const size_t items = (size_t)n * p->B, it0 = (size_t)f0 * p->B;
+  if (dct) HIP_TRY(hipMemcpy(dct, p->ws.dct + (size_t)f0 * p->N, sizeof(double) * n * (size_t)p->N, hipMemcpyDeviceToHost));
+  if (r) HIP_TRY(hipMemcpy(r, p->ws.r + it0 * p->nlags, sizeof(double) * items * p->nlags, hipMemcpyDeviceToHost));
+  if (a) HIP_TRY(hipMemcpy(a, p->ws.a + it0 * (p->p + 1), sizeof(double) * items * (p->p + 1), hipMemcpyDeviceToHost));
+  if (gg) HIP_TRY(hipMemcpy(gg, p->ws.gg + it0, sizeof(double) * items, hipMemcpyDeviceToHost));
+  if (cep) HIP_TRY(hipMemcpy(cep, p->ws.cep + it0 * p->M, sizeof(double) * items * p->M, hipMemcpyDeviceToHost));
+  if (env) HIP_TRY(hipMemcpy(env, p->ws.env + it0 * p->kk, sizeof(double) * items * p->kk, hipMemcpyDeviceToHost));
+  return FDLP_OK;
+}
+
 int fdlp_debug_fetch(fdlp_plan* p, int32_t n, double* dct, double* r, double* a, double* gg, double* cep,
                      double* env) {
-  if (!p || n < 0 || n > p->max_frames || p->device < 0) return fail(FDLP_E_INVALID, "fdlp_debug_fetch: bad args");
-  HIP_TRY(hipDeviceSynchronize());
-  const size_t items = (size_t)n * p->B;
-  if (dct) HIP_TRY(hipMemcpy(dct, p->ws.dct, sizeof(double) * n * (size_t)p->N, hipMemcpyDeviceToHost));
-  if (r) HIP_TRY(hipMemcpy(r, p->ws.r, sizeof(double) * items * p->nlags, hipMemcpyDeviceToHost));
-  if (a) HIP_TRY(hipMemcpy(a, p->ws.a, sizeof(double) * items * (p->p + 1), hipMemcpyDeviceToHost));
-  if (gg) HIP_TRY(hipMemcpy(gg, p->ws.gg, sizeof(double) * items, hipMemcpyDeviceToHost));
-  if (cep) HIP_TRY(hipMemcpy(cep, p->ws.cep, sizeof(double) * items * p->M, hipMemcpyDeviceToHost));
-  if (env) HIP_TRY(hipMemcpy(env, p->ws.env, sizeof(double) * items * p->kk, hipMemcpyDeviceToHost));
-  return FDLP_OK;
+  return fdlp_debug_fetch_range(p, 0, n, dct, r, a, gg, cep, env);
 }
 
 int fdlp_dct_rows(fdlp_plan* p, const double* x, int32_t n, double* y, void* stream) {
@@ -1112,7 +1146,8 @@ int fdlp_mel_plan_create(const fdlp_mel_config* cfg, int device, fdlp_mel_plan**
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) MEL_FAIL(FDLP_E_HIP, "no HIP device visible");
   if (device >= ndev) MEL_FAIL(FDLP_E_INVALID, "device index out of range");
-  if (hipSetDevice(device) != hipSuccess) MEL_FAIL(FDLP_E_HIP, "hipSetDevice failed");
+  DeviceGuard dg(device);
+  if (dg.status() != hipSuccess) MEL_FAIL(FDLP_E_HIP, "hipSetDevice failed");
   MEL_TRY(upload(&p->d_win, win.data(), win.size()));
   MEL_TRY(upload(&p->d_fb, fb.data(), fb.size()));
   MEL_TRY(upload(&p->d_lo, lo.data(), lo.size()));

@@ -272,13 +272,17 @@ class FdlpPlan:
     def set_debug(self, keep_intermediates: bool = True):
         check(lib.fdlp_set_debug(self._h, int(bool(keep_intermediates))))
 
-    def debug_fetch(self, n_frames: int):
+    def debug_fetch(self, n_frames: int, first_frame: int = 0, keys=("dct", "r", "a", "gg", "cep", "env")):
+        """Intermediates of frames [first_frame, first_frame + n_frames) of the last batch; a/gg/cep
+        need set_debug(True) before the compute."""
         F, B = int(n_frames), self.B
         p, M = int(self.cfg.order), int(self.cfg.coeff_num)
-        d = dict(dct=np.empty((F, self.N)), r=np.empty((F, B, self.nlags)), a=np.empty((F, B, p + 1)),
-                 gg=np.empty((F, B)), cep=np.empty((F, B, M)), env=np.empty((F, B, self.kk)))
-        check(lib.fdlp_debug_fetch(self._h, F, *[ptr(d[k], ctypes.c_double)
-                                                 for k in ("dct", "r", "a", "gg", "cep", "env")]))
+        shapes = dict(dct=(F, self.N), r=(F, B, self.nlags), a=(F, B, p + 1), gg=(F, B), cep=(F, B, M),
+                      env=(F, B, self.kk))
+        d = {k: np.empty(shapes[k]) for k in keys}
+        check(lib.fdlp_debug_fetch_range(self._h, int(first_frame), F,
+                                         *[ptr(d[k], ctypes.c_double) if k in d else None
+                                           for k in ("dct", "r", "a", "gg", "cep", "env")]))
         return d
 
     def set_profiling(self, enable: bool = True):

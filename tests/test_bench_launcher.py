@@ -1,0 +1,43 @@
+"""bench.py's N > 1 path on the CPU: `--gpus N` without a launcher starts N rank processes itself,
+every rank takes a contiguous split_scp shard of the synthetic scp (make_FDLPspectrum_feats.sh:135-157),
+ranks meet over gloo for the barrier and the max-of-elapsed only, and rank 0 prints one JSON line.
+--dry-run skips the device work and keeps the launcher, the sharding and the reduction."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--steps", "2", "--warmup", "1"]
+                       + list(extra), cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("gpus", [1, 2, 3])
+def test_dry_run_shards_cover_scp(gpus):
+    res = _run("--gpus", str(gpus), "--utts", "5")
+    assert res["n_gpus"] == gpus and res["dry_run"]
+    assert res["scp_entries"] == 5 * gpus
+    shards = res["shards"]
+    assert len(shards) == gpus
+    assert shards[0][0] == 0 and shards[-1][1] == res["scp_entries"]
+    for (a0, a1, fa), (b0, b1, fb) in zip(shards, shards[1:]):
+        assert a1 == b0 and a0 < a1                      # contiguous, disjoint, non-empty
+    assert all(f == 5 * 4 for _, _, f in shards)         # 5 utterances x 4 frames of 4 s each
+
+
+def test_dry_run_librispeech_shards_balance_frames():
+    res = _run("--gpus", "2", "--workload", "librispeech", "--frames", "300")
+    shards = res["shards"]
+    assert shards[0][1] == shards[1][0] and shards[1][1] == res["scp_entries"]
+    tot = sum(f for _, _, f in shards)
+    assert tot <= 600 and all(f >= 0.3 * tot for _, _, f in shards)
