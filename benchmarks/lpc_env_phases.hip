@@ -40,6 +40,7 @@ int main(int argc, char** argv) {
   fdlp::DevConsts c{};
   c.p = p; c.nlags = nlags; c.M = M; c.Me = M; c.kk = kk; c.env_nfft = env_nfft;
   c.weights = d_w; c.env_cos = d_cos; c.env_win = d_win;
+  CK(fdlp::prepare_lpc_env(c));  // lattice kernel launch geometry (FDLP_LPC_SLOTMAJOR / FDLP_LPC_LDS read here)
   hipStream_t s;
   CK(hipStreamCreate(&s));
   for (int i = 0; i < 3; ++i) CK(fdlp::launch_lpc_env(c, 0, d_r, items, d_env, nullptr, nullptr, nullptr, s));

@@ -1697,6 +1697,111 @@ __device__ __forceinline__ void lattice_durbin(double (&A)[SL], double (&B)[SL],
   if constexpr (Q + 1 < SL) lattice_durbin<SL, Q + 1>(A, B, R1, E, p, lane0);
 }
 
+// -----------------------------------------------------------------------------------------
+// Durbin in lattice form with CONTIGUOUS chunks: in phase S (orders k < 16 S) lane l of the row owns
+// positions l S .. l S + S - 1 of A = a^(k), of the mirror B (b_m = a^(k)_{k-m}) and of R1 (r_{m+1}).
+// The one-position shift z B of the lattice update then moves data between lanes only at the chunk
+// boundary: one DPP row_shr:1 of the last slot per order (bound_ctrl: lane 0 takes 0), and the
+// in-lane part of the shift is free because B alternates between two register banks (the new B[j] is
+// written from the old B[j-1]).  Per order: 3 S FMAs (update of A and B, next order's dot product)
+// + the 16-lane reduction + the 1/E Newton steps, instead of the slot-major layout's 3 S FMAs + 3 S
+// DPP moves.  Capacity grows with k: every 16 orders A and B are re-laid out through the item's LDS
+// scratch (S -> S + 1 positions per lane) and R1 is reloaded for the new layout (prefetched from
+// global memory one phase ahead).  Same recursion as lattice_phase (features.py:226-228): both halves
+// of every symmetric pair are fma(kappa, a_{k-i}, a_i).
+// -----------------------------------------------------------------------------------------
+template <int S>
+__device__ __forceinline__ void contig_step(double (&A)[S], const double (&Bs)[S], double (&Bd)[S],
+                                            const double (&R1)[S], double& part, double& E) {
+  const double acc = row_sum16(part);  // r_k + sum_i a_i r_{k-i} = sum_m b_m r_{m+1}
+  double rE = __builtin_amdgcn_rcp(E);
+  rE = fma(rE, fma(-E, rE, 1.0), rE);
+  rE = fma(rE, fma(-E, rE, 1.0), rE);
+  const double kappa = -acc * rE;
+  // z B at slot 0: the last slot of lane l-1 (row_shr:1); lane 0 takes 0 (bound_ctrl)
+  const double z0 = __builtin_amdgcn_update_dpp(0.0, Bs[S - 1], 0x111, 0xF, 0xF, true);
+  double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const double zb = j == 0 ? z0 : Bs[j - 1];
+    Bd[j] = fma(kappa, A[j], zb);
+    A[j] = fma(kappa, zb, A[j]);
+    if (j & 1) p1 = fma(Bd[j], R1[j], p1);
+    else p0 = fma(Bd[j], R1[j], p0);
+  }
+  part = p0 + p1;
+  E = E * (1.0 - kappa * kappa);
+}
+
+// R1 of phase S for lane l: r_{lS+j+1} for positions <= p, 0 beyond (and for invalid items)
+template <int S>
+__device__ __forceinline__ void contig_load_r1(double (&R1)[S], const double* rr, int nlags, int p, int l, bool valid) {
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int m = l * S + j;
+    const double v = rr[min(m + 1, nlags - 1)];
+    R1[j] = (valid && m <= p) ? v : 0.0;
+  }
+}
+
+// vec (S per lane, contiguous) -> la -> out (S + 1 per lane); positions >= 16 S read as 0
+template <int S>
+__device__ __forceinline__ void contig_relayout(const double (&v)[S], double (&out)[S + 1], double* la, int l) {
+  wave_lds_sync();
+#pragma unroll
+  for (int j = 0; j < S; ++j) la[l * S + j] = v[j];
+  la[16 * S + l] = 0.0;
+  wave_lds_sync();
+#pragma unroll
+  for (int j = 0; j <= S; ++j) out[j] = la[l * (S + 1) + j];
+}
+
+// Orders k in [k0, k1) of phase S, then the next phase (or, after order p, the final A in place).
+template <int SL, int S>
+__device__ __forceinline__ void contig_durbin(double (&A)[S], double (&B)[S], double (&R1)[S], double& part,
+                                              double& E, double* la, const double* rr, int nlags, int p, int l,
+                                              bool valid, double& gg, double r0) {
+  const int k0 = S == 1 ? 1 : 16 * (S - 1);
+  const int k1 = min(p + 1, 16 * S);
+  constexpr int SN = S < SL ? S + 1 : S;
+  double R1n[SN];
+  if constexpr (S < SL) {
+    if (k1 <= p) contig_load_r1<SN>(R1n, rr, nlags, p, l, valid);  // next phase's R1, consumed after the loop
+  }
+  double B2[S];
+  int k = k0;
+  for (; k + 1 < k1; k += 2) {
+    contig_step<S>(A, B, B2, R1, part, E);
+    contig_step<S>(A, B2, B, R1, part, E);
+  }
+  if (k < k1) {
+    contig_step<S>(A, B, B2, R1, part, E);
+#pragma unroll
+    for (int j = 0; j < S; ++j) B[j] = B2[j];
+  }
+  if constexpr (S < SL) {
+    if (k1 <= p) {
+      double An[S + 1], Bn[S + 1];
+      contig_relayout<S>(A, An, la, l);
+      contig_relayout<S>(B, Bn, la, l);
+      contig_durbin<SL, S + 1>(An, Bn, R1n, part, E, la, rr, nlags, p, l, valid, gg, r0);
+      return;
+    }
+  }
+  // order p done: gg = r0 + sum_{m=0}^{p} a_m r_{m+1} (the reference's off-by-one, features.py:228);
+  // A goes to la[0 .. 16 S) in position order for the cepstrum (zeros beyond p)
+  double q0 = 0.0, q1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    if (j & 1) q1 = fma(A[j], R1[j], q1);
+    else q0 = fma(A[j], R1[j], q0);
+  }
+  gg = r0 + row_sum16(q0 + q1);
+  wave_lds_sync();
+#pragma unroll
+  for (int j = 0; j < S; ++j) la[l * S + j] = A[j];
+}
+
 // lpc_env with the lattice Durbin: persistent waves (grid-stride over groups of 4 items), r read
 // straight into registers, LDS only for a (cepstrum) and c (envelope).  Same outputs as lpc_env_kernel.
 constexpr int kEnvChunk = 5;  // envelope slots held in registers at a time
@@ -1704,7 +1809,9 @@ constexpr int kEnvChunk = 5;  // envelope slots held in registers at a time
 // computed it (v_fmac_f64_dpp row_newbcast, the broadcast is the FMA's source modifier) instead of an
 // LDS read per term: one LDS read (alpha_{n-k}) and one FMA per term instead of two reads, a multiply
 // and an FMA.  CB = 0: the LDS form for any M.
-template <int SL, int CB = 0>
+// CONTIG: the contiguous-chunk Durbin (contig_durbin, default); otherwise the slot-major lattice
+// (lattice_durbin, FDLP_LPC_SLOTMAJOR=1).
+template <int SL, int CB = 0, bool CONTIG = true>
 #ifndef FDLP_LAT_WAVES
 #define FDLP_LAT_WAVES 4  // waves per SIMD the lattice kernel is compiled for (register budget)
 #endif
@@ -1714,12 +1821,14 @@ __global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(Lpc
   const int ngroups = (A.items + 3) >> 2;
   // (prefetching the next group's r into registers before the envelope phase was measured: no gain,
   // it costs a wave per SIMD of occupancy)
-  double Rn[SL], r0n;
+  double Rn[CONTIG ? 1 : SL], r0n;
   auto load_r = [&](int grp) {
     const int it = grp * 4 + (threadIdx.x >> 4);
     const double* rr = A.r + (int64_t)(it < A.items ? it : 0) * A.nlags;
+    if constexpr (!CONTIG) {
 #pragma unroll
-    for (int s = 0; s < SL; ++s) Rn[s] = rr[min((int)(threadIdx.x & 15) + 16 * s + 1, A.nlags - 1)];
+      for (int s = 0; s < SL; ++s) Rn[s] = rr[min((int)(threadIdx.x & 15) + 16 * s + 1, A.nlags - 1)];
+    }
     r0n = rr[0];
   };
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
@@ -1740,30 +1849,51 @@ __global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(Lpc
     const int item = grp * 4 + g;
     const bool valid = item < A.items;
     // ---- phase 1: Levinson-Durbin (features.py:226-228) in registers -------------------------
-    double Av[SL], Bv[SL], R1[SL];
+    double gg;
+    if constexpr (CONTIG) {
+      const double* rr = A.r + (int64_t)(valid ? item : 0) * A.nlags;
+      const double r0 = valid ? r0n : 1.0;
+      gg = r0;
+      {
+        double A1[1] = {lane0 ? 1.0 : 0.0}, B1[1] = {lane0 ? 1.0 : 0.0}, R11[1];
+        contig_load_r1<1>(R11, rr, A.nlags, p, l, valid);
+        double part = lane0 ? R11[0] : 0.0;  // order 1: b^(0) . R1 = r_1
+        double E = r0;
+        if (FDLP_LPC_PHASES & 1) contig_durbin<SL, 1>(A1, B1, R11, part, E, la, rr, A.nlags, p, l, valid, gg, r0);
+      }
+      // la[0 .. 16 SL) holds a_0 .. a_p (zeros beyond p); zero the rest of the a region
+      for (int q = l + 16 * SL; q < NAL; q += 16) la[q] = 0.0;
+      wave_lds_sync();
+      if (valid && A.a_out) {
+        for (int m = l; m <= p; m += 16) A.a_out[(int64_t)item * (p + 1) + m] = la[m];
+        if (lane0) A.gg_out[item] = gg;
+      }
+    } else {
+      double Av[SL], Bv[SL], R1[SL];
 #pragma unroll
-    for (int s = 0; s < SL; ++s) {  // branch-free: clamped loads (load_r), then select
-      const int m = l + 16 * s;
-      R1[s] = (valid && m <= p) ? Rn[s] : 0.0;
-      Av[s] = (m == 0) ? 1.0 : 0.0;
-      Bv[s] = Av[s];
+      for (int s = 0; s < SL; ++s) {  // branch-free: clamped loads (load_r), then select
+        const int m = l + 16 * s;
+        R1[s] = (valid && m <= p) ? Rn[s] : 0.0;
+        Av[s] = (m == 0) ? 1.0 : 0.0;
+        Bv[s] = Av[s];
+      }
+      const double r0 = valid ? r0n : 1.0;
+      double E = r0;
+      if (FDLP_LPC_PHASES & 1) lattice_durbin<SL, 0>(Av, Bv, R1, E, p, lane0);
+      double part = 0.0;
+#pragma unroll
+      for (int s = 0; s < SL; ++s) part = fma(Av[s], R1[s], part);
+      gg = r0 + row_sum16(part);  // the reference's off-by-one gain (features.py:228)
+      wave_lds_sync();  // the previous group's envelope reads of la are done
+#pragma unroll
+      for (int s = 0; s < SL; ++s) {
+        const int m = l + 16 * s;
+        if (m < NAL) la[m] = m <= p ? Av[s] : 0.0;
+        if (valid && A.a_out && m <= p) A.a_out[(int64_t)item * (p + 1) + m] = Av[s];
+      }
+      for (int q = l + 16 * SL; q < NAL; q += 16) la[q] = 0.0;
+      if (valid && A.a_out && lane0) A.gg_out[item] = gg;
     }
-    const double r0 = valid ? r0n : 1.0;
-    double E = r0;
-    if (FDLP_LPC_PHASES & 1) lattice_durbin<SL, 0>(Av, Bv, R1, E, p, lane0);
-    double part = 0.0;
-#pragma unroll
-    for (int s = 0; s < SL; ++s) part = fma(Av[s], R1[s], part);
-    const double gg = r0 + row_sum16(part);  // the reference's off-by-one gain (features.py:228)
-    wave_lds_sync();  // the previous group's envelope reads of la are done
-#pragma unroll
-    for (int s = 0; s < SL; ++s) {
-      const int m = l + 16 * s;
-      if (m < NAL) la[m] = m <= p ? Av[s] : 0.0;
-      if (valid && A.a_out && m <= p) A.a_out[(int64_t)item * (p + 1) + m] = Av[s];
-    }
-    for (int q = l + 16 * SL; q < NAL; q += 16) la[q] = 0.0;
-    if (valid && A.a_out && lane0) A.gg_out[item] = gg;
     wave_lds_sync();
     // ---- phase 2: cepstrum (features.py:233-246), as in lpc_env_kernel -------------------------
     if constexpr (CB > 0) {
@@ -2321,7 +2451,7 @@ int lpc_env_region(int p, int M) {
 // Lattice-kernel instantiation of a plan: calls fn(integral_constant<SL>, integral_constant<CB>) or
 // returns hipErrorNotSupported when the plan runs the LDS Durbin (lpc_env_kernel).
 template <class Fn>
-static hipError_t lattice_dispatch(const DevConsts& c, Fn&& fn) {
+static hipError_t lattice_dispatch_sl(const DevConsts& c, Fn&& fn) {
   using std::integral_constant;
   const int SL = (c.p + 1 + 15) / 16;
   if (SL > 16 || c.lpc_lds_durbin) return hipErrorNotSupported;
@@ -2343,6 +2473,16 @@ static hipError_t lattice_dispatch(const DevConsts& c, Fn&& fn) {
   }
 }
 
+// fn(integral_constant<SL>, integral_constant<CB>, integral_constant<bool, CONTIG>)
+template <class Fn>
+static hipError_t lattice_dispatch(const DevConsts& c, Fn&& fn) {
+  using std::integral_constant;
+  return lattice_dispatch_sl(c, [&](auto sl, auto cb) -> hipError_t {
+    if (c.lpc_slotmajor) return fn(sl, cb, integral_constant<bool, false>{});
+    return fn(sl, cb, integral_constant<bool, true>{});
+  });
+}
+
 static size_t lattice_lds(const DevConsts& c) {
   const int NAL = (c.M > c.p + 1 ? c.M : c.p + 1) + 16;
   const int region = (NAL + c.M + 15) / 32 * 32 + 16;  // = 16 mod 32 doubles (disjoint bank halves per item)
@@ -2352,6 +2492,7 @@ static size_t lattice_lds(const DevConsts& c) {
 hipError_t prepare_lpc_env(DevConsts& c) {
   c.lpc_lds_durbin = getenv("FDLP_LPC_LDS") != nullptr;
   c.lpc_cep_lds = getenv("FDLP_CEP_LDS") != nullptr;
+  c.lpc_slotmajor = getenv("FDLP_LPC_SLOTMAJOR") != nullptr;
   c.lpc_blocks = 0;
   int dev = 0, cus = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -2359,14 +2500,15 @@ hipError_t prepare_lpc_env(DevConsts& c) {
   if (e != hipSuccess) return e;
   const size_t lds = lattice_lds(c);
   int per_cu = 0;
-  e = lattice_dispatch(c, [&](auto sl, auto cb) -> hipError_t {
+  e = lattice_dispatch(c, [&](auto sl, auto cb, auto ct) -> hipError_t {
     constexpr int SL = decltype(sl)::value, CB = decltype(cb)::value;
+    constexpr bool CT = decltype(ct)::value;
     if (lds > 65536) {
-      const hipError_t a = hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL, CB>,
+      const hipError_t a = hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL, CB, CT>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (a != hipSuccess) return a;
     }
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lpc_env_lattice_kernel<SL, CB>, 64, lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lpc_env_lattice_kernel<SL, CB, CT>, 64, lds);
   });
   if (e == hipErrorNotSupported) return hipSuccess;  // LDS Durbin: one block per item group, no setup
   if (e != hipSuccess) return e;
@@ -2386,9 +2528,10 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
     const size_t lds = lattice_lds(c);
     A.region = (int)(lds / (4 * sizeof(double)));
     const int grid = std::min((items + 3) / 4, c.lpc_blocks);
-    return lattice_dispatch(c, [&](auto sl, auto cb) -> hipError_t {
+    return lattice_dispatch(c, [&](auto sl, auto cb, auto ct) -> hipError_t {
       constexpr int SL = decltype(sl)::value, CB = decltype(cb)::value;
-      hipLaunchKernelGGL((lpc_env_lattice_kernel<SL, CB>), dim3(grid), dim3(64), lds, s, A);
+      constexpr bool CT = decltype(ct)::value;
+      hipLaunchKernelGGL((lpc_env_lattice_kernel<SL, CB, CT>), dim3(grid), dim3(64), lds, s, A);
       return hipGetLastError();
     });
   }
