@@ -4,7 +4,8 @@ including the host side the device-resident bench.py excludes: WAV read + parse,
 D2H and the ark writer.  Synthetic speech-like 4 s WAVs (bench.speech_like_batch) in a temp dir.
 
     python benchmarks/cli_throughput.py [--utts 512] [--workers 1 4 8] [--batch-frames 8192]
-Prints one JSON line per worker count.
+                                        [--runners native python]
+Prints one JSON line per (host runner, worker count).
 """
 import argparse
 import json
@@ -27,6 +28,7 @@ def main():
     ap.add_argument("--workers", type=int, nargs="+", default=[1, 4, 8])
     ap.add_argument("--batch-frames", type=int, default=8192)
     ap.add_argument("--profile", default=None, help="write cProfile stats of the last run to this file")
+    ap.add_argument("--runners", nargs="+", default=["native", "python"], choices=["native", "python"])
     a = ap.parse_args()
     from bench import speech_like_batch
     from speech_recognition_tools_amd.featgen.computeFDLPSpectrogram import build_parser, getFeats
@@ -48,9 +50,9 @@ def main():
         getFeats(build_parser().parse_args([os.path.join(d, "wav.scp"), os.path.join(d, "warm")] + opts),
                  return_feats=False)
         sys.stdout = so
-        for w in a.workers:
+        for runner, w in [(r, w) for r in a.runners for w in a.workers]:
             args = build_parser().parse_args([os.path.join(d, "wav.scp"), os.path.join(d, "o%d" % w),
-                                              "--io_workers=%d" % w] + opts)
+                                              "--io_workers=%d" % w, "--host_runner=" + runner] + opts)
             sys.stdout = devnull
             prof = None
             if a.profile:
@@ -70,6 +72,7 @@ def main():
             audio_h = a.utts * T / 16000.0 / 3600.0
             print(json.dumps({"metric": "compute-fdlp-feats end-to-end audio-hours/s (WAV in, ark out)",
                               "value": audio_h / el, "unit": "audio-hours/s", "io_workers": w,
+                              "host_runner": runner,
                               "utts": a.utts, "utt_seconds": a.seconds, "seconds": el,
                               "ark_bytes": os.path.getsize(os.path.join(d, "o%d.ark" % w))}))
             sys.stdout.flush()

@@ -278,8 +278,15 @@ int fdlp_noise_params(const int16_t* sig, int64_t T, const int16_t* noise, int64
 /* Parse a RIFF/WAVE PCM16 mono buffer.  *samples points into `buf`. */
 int fdlp_wav_parse(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* channels,
                    const int16_t** samples, int64_t* n_samples);
+/* Any RIFF/RIFX WAVE buffer scipy.io.wavfile.read accepts (PCM 1-64 bit, <= 8 bit unsigned, 3/5/6/7-byte
+ * containers left-justified; IEEE float 32/64; WAVE_FORMAT_EXTENSIBLE): sample rate, channels, frames, and
+ * *is_int16 = 1 when scipy would return int16.  With out != NULL the interleaved samples are written as
+ * the double values of scipy's array (ABI 3). */
+int fdlp_wav_decode(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* channels, int32_t* is_int16,
+                    int64_t* n_samples, double* out);
 typedef struct fdlp_ark_writer fdlp_ark_writer;
-/* Kaldi binary ark + scp ("<utt> <abs ark path>:<offset>") like `copy-feats ark,t:- ark,scp:`. */
+/* Kaldi binary ark + scp ("<utt> <abs ark path>:<offset>") like `copy-feats ark,t:- ark,scp:`.  Written to
+ * <path>.tmp and renamed to <path> by fdlp_ark_close (removed instead after a failed write). */
 int fdlp_ark_open(const char* ark_path, const char* scp_path, fdlp_ark_writer** out);
 int fdlp_ark_write(fdlp_ark_writer* w, const char* utt, const float* mat, int32_t rows,
                    int32_t cols);
@@ -298,6 +305,40 @@ int fdlp_mat_reader_close(fdlp_mat_reader* r);
  * + row-major fp64, or Kaldi text " [\n  v v ... \n  v v ... ]\n" (%g, the ostream default). */
 int fdlp_kaldi_write_dmatrix(const char* path, const double* m, int32_t rows, int32_t cols,
                              int32_t binary);
+
+/* ---- native JOB runner (getFeats' utterance loop, computeFDLPSpectrogram.py:119-237) --------- */
+/* One scp shard end to end: reader threads (files, `<cmd> |` pipes, `<ark>:<offset>` wave entries,
+ * scipy's WAV formats), the reference's skip / sample-rate semantics, noise offsets and hop jitter from
+ * the RNG replicas, device batches of <= batch_frames frames through fdlp_compute (copies and kernels of
+ * consecutive batches overlapped), and a writer thread for <outfile>.ark/.scp (and .len), each written
+ * to <name>.tmp and renamed when complete.  Progress lines go to stdout like the reference's (:185). */
+typedef struct fdlp_job_opts {
+  int32_t scp_type;            /* 0 wav, 1 segment (both read natively; no wav-copy needed)           */
+  int32_t write_len;           /* --write_utt2num_frames                                               */
+  int32_t ark_decimals;        /* '%.3f' text-ark rounding of the reference (3); <0 keeps float32      */
+  int32_t batch_frames;        /* analysis frames per device batch (a longer utterance grows the plan) */
+  int32_t io_threads;          /* reader threads                                                       */
+  int32_t preprocess;          /* FDLP_PRE_NONE | FDLP_PRE_DIFF (--add_noise diff)                     */
+  const int16_t* noise;        /* nullable host noise samples (--add_noise <type>,<snr>)              */
+  int64_t noise_len;
+  double snr;
+  uint32_t noise_seed;         /* numpy legacy seed of the noise offsets (np.random.rand, features.py:25) */
+  const uint32_t* jitter_key;  /* CPython random.seed key words of the hop jitter (:225)              */
+  int32_t jitter_key_len;
+  int32_t srate;               /* the sample rate the reference asserts (16000, :144)                 */
+  const char* progress_name;   /* non-NULL: "<name>: Computing Features for file: <utt>" per utterance */
+  const char* cmvn_path;       /* non-NULL: global CMVN stats (Kaldi binary DM) of the written features */
+} fdlp_job_opts;
+typedef struct fdlp_job_stats {
+  int64_t n_lines;             /* scp entries                                  */
+  int64_t n_done;              /* utterances featurised                        */
+  int64_t n_skipped;           /* unreadable entries skipped (:135-142)         */
+  int64_t n_frames_out;        /* feature rows written                         */
+  int64_t n_samples;           /* samples featurised                           */
+  double seconds;              /* wall time of the call                        */
+} fdlp_job_stats;
+int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_path, const char* outfile,
+                 const fdlp_job_opts* opts, fdlp_job_stats* stats);
 
 #ifdef __cplusplus
 }

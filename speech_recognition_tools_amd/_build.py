@@ -7,7 +7,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libfdlp_hip.so")
-SOURCES = ["fdlp_kernels.hip", "fdlp_plan.cpp", "fdlp_host.cpp"]
+SOURCES = ["fdlp_kernels.hip", "fdlp_plan.cpp", "fdlp_host.cpp", "fdlp_job.cpp"]
 HEADERS = ["fdlp_internal.h", "fdlp_error.h", os.path.join("..", "..", "include", "fdlp.h")]
 ARCH = os.environ.get("FDLP_OFFLOAD_ARCH", "gfx950")
 

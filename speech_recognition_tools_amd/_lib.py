@@ -83,6 +83,22 @@ class FdlpReverbBatchC(ctypes.Structure):
     ]
 
 
+class FdlpJobOptsC(ctypes.Structure):
+    _fields_ = [
+        ("scp_type", c_i32), ("write_len", c_i32), ("ark_decimals", c_i32), ("batch_frames", c_i32),
+        ("io_threads", c_i32), ("preprocess", c_i32), ("noise", P_i16), ("noise_len", c_i64), ("snr", c_dbl),
+        ("noise_seed", ctypes.c_uint32), ("jitter_key", P_u32), ("jitter_key_len", c_i32), ("srate", c_i32),
+        ("progress_name", ctypes.c_char_p), ("cmvn_path", ctypes.c_char_p),
+    ]
+
+
+class FdlpJobStatsC(ctypes.Structure):
+    _fields_ = [
+        ("n_lines", c_i64), ("n_done", c_i64), ("n_skipped", c_i64), ("n_frames_out", c_i64),
+        ("n_samples", c_i64), ("seconds", c_dbl),
+    ]
+
+
 # name -> (restype, argtypes); every function declared in include/fdlp.h
 SIGNATURES = {
     "fdlp_plan_create": (c_i32, [ctypes.POINTER(FdlpConfigC), c_i32, ctypes.POINTER(c_p)]),
@@ -118,6 +134,9 @@ SIGNATURES = {
     "fdlp_nprandom_destroy": (c_i32, [c_p]),
     "fdlp_noise_params": (c_i32, [P_i16, c_i64, P_i16, c_i64, c_dbl, c_dbl, P_i64, P_dbl]),
     "fdlp_wav_parse": (c_i32, [P_u8, c_i64, P_i32, P_i32, ctypes.POINTER(P_i16), P_i64]),
+    "fdlp_wav_decode": (c_i32, [P_u8, c_i64, P_i32, P_i32, P_i32, P_i64, P_dbl]),
+    "fdlp_job_run": (c_i32, [ctypes.POINTER(FdlpConfigC), c_i32, ctypes.c_char_p, ctypes.c_char_p,
+                             ctypes.POINTER(FdlpJobOptsC), ctypes.POINTER(FdlpJobStatsC)]),
     "fdlp_ark_open": (c_i32, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(c_p)]),
     "fdlp_ark_write": (c_i32, [c_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), c_i32, c_i32]),
     "fdlp_ark_close": (c_i32, [c_p]),

@@ -4,8 +4,8 @@
 //   * numpy legacy RandomState replica (init_genrand + 53-bit rand())      -> noise offset
 //     (features.py:25)
 //   * add_noise_to_wav energies with int16-wrapped squares                  (features.py:24-31)
-//   * RIFF/WAVE PCM16 parser                          (replaces scipy.io.wavfile.read, :133,:139)
-//   * Kaldi binary ark/scp writer               (replaces dict2Ark + copy-feats, features.py:63-69)
+//   * RIFF/WAVE parser with scipy.io.wavfile.read's formats   (replaces scipy's read, :133,:139)
+//   * Kaldi binary ark/scp writer, tmp + rename  (replaces dict2Ark + copy-feats, features.py:63-69)
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -157,43 +157,128 @@ int fdlp_noise_params(const int16_t* sig, int64_t T, const int16_t* noise, int64
 static uint32_t rd32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
 static uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
 
-int fdlp_wav_parse(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* channels, const int16_t** samples,
-                   int64_t* n_samples) {
-  if (!buf || len < 12 || memcmp(buf, "RIFF", 4) || memcmp(buf + 8, "WAVE", 4))
+// The data chunk of a RIFF/RIFX/WAVE buffer and its format, as scipy.io.wavfile.read sees it
+// (scipy/io/wavfile.py _read_fmt_chunk / _read_data_chunk): PCM of 1..64 bits (<= 8 bits unsigned,
+// 3/5/6/7-byte containers left-justified into int32/int64), IEEE float 32/64, WAVE_FORMAT_EXTENSIBLE.
+struct WavInfo {
+  int32_t sr = 0, ch = 0;
+  int fmt = 0, bits = 0, bps = 0;  // format tag, bits per sample, container bytes per sample
+  bool big = false;
+  const uint8_t* data = nullptr;
+  int64_t frames = 0;  // samples per channel
+};
+
+static uint32_t rdu32(const uint8_t* p, bool big) {
+  return big ? ((uint32_t)p[0] << 24 | p[1] << 16 | p[2] << 8 | p[3]) : rd32(p);
+}
+static uint16_t rdu16(const uint8_t* p, bool big) { return big ? (uint16_t)(p[0] << 8 | p[1]) : rd16(p); }
+
+static int wav_info(const uint8_t* buf, int64_t len, WavInfo* w) {
+  if (!buf || len < 12 || (memcmp(buf, "RIFF", 4) && memcmp(buf, "RIFX", 4)) || memcmp(buf + 8, "WAVE", 4))
     return fdlp::fail(FDLP_E_IO, "not a RIFF/WAVE buffer");
+  w->big = !memcmp(buf, "RIFX", 4);
   int64_t pos = 12;
-  int fmt_ok = 0;
-  uint16_t fmt = 0, ch = 0, bits = 0;
-  uint32_t sr = 0;
+  int fmt_ok = 0, block_align = 0;
   while (pos + 8 <= len) {
     const uint8_t* h = buf + pos;
-    uint32_t sz = rd32(h + 4);
+    const uint32_t sz = rdu32(h + 4, w->big);
     const int64_t body = pos + 8;
     if (!memcmp(h, "fmt ", 4)) {
       if (sz < 16 || body + 16 > len) return fdlp::fail(FDLP_E_IO, "truncated fmt chunk");
-      fmt = rd16(buf + body);
-      ch = rd16(buf + body + 2);
-      sr = rd32(buf + body + 4);
-      bits = rd16(buf + body + 14);
-      if (fmt == 0xFFFE && sz >= 40) fmt = rd16(buf + body + 24);  // WAVE_FORMAT_EXTENSIBLE subformat
+      w->fmt = rdu16(buf + body, w->big);
+      w->ch = rdu16(buf + body + 2, w->big);
+      w->sr = (int32_t)rdu32(buf + body + 4, w->big);
+      block_align = rdu16(buf + body + 12, w->big);
+      w->bits = rdu16(buf + body + 14, w->big);
+      if (w->fmt == 0xFFFE && sz >= 18) {  // WAVE_FORMAT_EXTENSIBLE: subformat GUID {XXXXXXXX-0000-0010-8000-00AA00389B71}
+        if (body + 18 > len || rdu16(buf + body + 16, w->big) < 22 || body + 40 > len)
+          return fdlp::fail(FDLP_E_IO, "Binary structure of wave file is not compliant");
+        static const uint8_t tail_le[12] = {0, 0, 0x10, 0, 0x80, 0, 0, 0xAA, 0, 0x38, 0x9B, 0x71};
+        static const uint8_t tail_be[12] = {0, 0, 0, 0x10, 0x80, 0, 0, 0xAA, 0, 0x38, 0x9B, 0x71};
+        if (!memcmp(buf + body + 28, w->big ? tail_be : tail_le, 12)) w->fmt = (int)rdu32(buf + body + 24, w->big);
+      }
       fmt_ok = 1;
     } else if (!memcmp(h, "data", 4)) {
       if (!fmt_ok) return fdlp::fail(FDLP_E_IO, "data chunk before fmt chunk");
-      if (fmt != 1 || bits != 16) return fdlp::fail(FDLP_E_IO, "only PCM16 WAV is supported");
-      int64_t avail = len - body;
-      // scipy tolerates an over-long size field (sox pipes write 0xFFFFFFFF): clamp
+      if (w->ch == 0) return fdlp::fail(FDLP_E_IO, "zero channels");
+      w->bps = block_align / w->ch;
+      if (w->bps < 1) return fdlp::fail(FDLP_E_IO, "block align smaller than the channel count");
+      if (w->fmt == 1) {
+        if (w->bits < 1 || w->bits > 64 || w->bps > 8) return fdlp::fail(FDLP_E_IO, "unsupported PCM bit depth");
+      } else if (w->fmt == 3) {
+        if ((w->bits != 32 && w->bits != 64) || (w->bps != 4 && w->bps != 8))
+          return fdlp::fail(FDLP_E_IO, "unsupported floating-point bit depth");
+      } else {
+        return fdlp::fail(FDLP_E_IO, "unknown wave format (only PCM and IEEE float are read)");
+      }
+      const int64_t avail = len - body;
+      // scipy reads what is there when the size field is larger (sox pipes write 0xFFFFFFFF)
       int64_t nbytes = (int64_t)sz > avail ? avail : (int64_t)sz;
       if (sz == 0 || sz == 0xFFFFFFFFu) nbytes = avail;
-      if (ch == 0) return fdlp::fail(FDLP_E_IO, "zero channels");
-      *srate = (int32_t)sr;
-      *channels = ch;
-      *samples = (const int16_t*)(buf + body);
-      *n_samples = nbytes / 2 / ch;
+      w->data = buf + body;
+      w->frames = nbytes / w->bps / w->ch;
       return FDLP_OK;
     }
     pos = body + sz + (sz & 1);
   }
   return fdlp::fail(FDLP_E_IO, "no data chunk");
+}
+
+// sample i (interleaved index) as the value scipy returns, converted to double
+static double wav_sample(const WavInfo& w, int64_t i) {
+  const uint8_t* p = w.data + i * w.bps;
+  if (w.fmt == 3) {
+    if (w.bps == 4) {
+      uint32_t u = rdu32(p, w.big);
+      float f;
+      memcpy(&f, &u, 4);
+      return (double)f;
+    }
+    uint64_t u = w.big ? ((uint64_t)rdu32(p, true) << 32 | rdu32(p + 4, true)) : ((uint64_t)rd32(p + 4) << 32 | rd32(p));
+    double d;
+    memcpy(&d, &u, 8);
+    return d;
+  }
+  if (w.bits <= 8) return (double)p[0];  // unsigned 8-bit (scipy 'u1')
+  // signed integer container of bps bytes; 3/5/6/7-byte containers are left-justified into 4/8 bytes
+  const int cont = (w.bps == 1 || w.bps == 2 || w.bps == 4 || w.bps == 8) ? w.bps : (w.bps == 3 ? 4 : 8);
+  uint64_t u = 0;
+  for (int b = 0; b < w.bps; ++b) {
+    const uint64_t byte = w.big ? p[b] : p[w.bps - 1 - b];  // most significant first
+    u = (u << 8) | byte;
+  }
+  u <<= 8 * (cont - w.bps);
+  const int sh = 64 - 8 * cont;
+  return (double)((int64_t)(u << sh) >> sh);
+}
+
+int fdlp_wav_parse(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* channels, const int16_t** samples,
+                   int64_t* n_samples) {
+  WavInfo w;
+  int rc = wav_info(buf, len, &w);
+  if (rc != FDLP_OK) return rc;
+  if (w.fmt != 1 || w.bits != 16 || w.bps != 2 || w.big) return fdlp::fail(FDLP_E_IO, "only PCM16 WAV is supported");
+  *srate = w.sr;
+  *channels = w.ch;
+  *samples = (const int16_t*)w.data;
+  *n_samples = w.frames;
+  return FDLP_OK;
+}
+
+int fdlp_wav_decode(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* channels, int32_t* is_int16,
+                    int64_t* n_samples, double* out) {
+  WavInfo w;
+  int rc = wav_info(buf, len, &w);
+  if (rc != FDLP_OK) return rc;
+  if (srate) *srate = w.sr;
+  if (channels) *channels = w.ch;
+  if (is_int16) *is_int16 = (w.fmt == 1 && w.bits > 8 && w.bps == 2 && !w.big) ? 1 : 0;
+  if (n_samples) *n_samples = w.frames;
+  if (out) {
+    const int64_t n = w.frames * w.ch;
+    for (int64_t i = 0; i < n; ++i) out[i] = wav_sample(w, i);
+  }
+  return FDLP_OK;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -202,29 +287,46 @@ int fdlp_wav_parse(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* cha
 struct fdlp_ark_writer {
   FILE* ark = nullptr;
   FILE* scp = nullptr;
-  std::string ark_abs;
+  std::string ark_abs;                   // absolute path of the final ark (what the scp lines name)
+  std::string ark_path, scp_path;        // final names
+  std::string ark_tmp, scp_tmp;          // written here, renamed by fdlp_ark_close
+  bool failed = false;
 };
+
+// absolute form of a path that may not exist yet: realpath of its directory + the file name
+static std::string abs_path(const std::string& p) {
+  const size_t slash = p.find_last_of('/');
+  const std::string dir = slash == std::string::npos ? "." : (slash == 0 ? "/" : p.substr(0, slash));
+  const std::string base = slash == std::string::npos ? p : p.substr(slash + 1);
+  char* d = realpath(dir.c_str(), nullptr);
+  std::string r = d ? std::string(d) + (std::string(d) == "/" ? "" : "/") + base : p;
+  free(d);
+  return r;
+}
 
 int fdlp_ark_open(const char* ark_path, const char* scp_path, fdlp_ark_writer** out) {
   if (!ark_path || !out) return fdlp::fail(FDLP_E_INVALID, "fdlp_ark_open: bad args");
   auto* w = new (std::nothrow) fdlp_ark_writer;
   if (!w) return fdlp::fail(FDLP_E_NOMEM, "fdlp_ark_open: out of memory");
-  w->ark = fopen(ark_path, "wb");
+  w->ark_path = ark_path;
+  w->ark_tmp = w->ark_path + ".tmp";
+  w->ark = fopen(w->ark_tmp.c_str(), "wb");
   if (!w->ark) {
     delete w;
     return fdlp::fail(FDLP_E_IO, std::string("cannot open ark ") + ark_path);
   }
   if (scp_path) {
-    w->scp = fopen(scp_path, "w");
+    w->scp_path = scp_path;
+    w->scp_tmp = w->scp_path + ".tmp";
+    w->scp = fopen(w->scp_tmp.c_str(), "w");
     if (!w->scp) {
       fclose(w->ark);
+      remove(w->ark_tmp.c_str());
       delete w;
       return fdlp::fail(FDLP_E_IO, std::string("cannot open scp ") + scp_path);
     }
   }
-  char* abs = realpath(ark_path, nullptr);
-  w->ark_abs = abs ? abs : ark_path;
-  free(abs);
+  w->ark_abs = abs_path(w->ark_path);
   *out = w;
   return FDLP_OK;
 }
@@ -232,7 +334,7 @@ int fdlp_ark_open(const char* ark_path, const char* scp_path, fdlp_ark_writer** 
 int fdlp_ark_write(fdlp_ark_writer* w, const char* utt, const float* mat, int32_t rows, int32_t cols) {
   if (!w || !utt || rows < 0 || cols < 0 || (rows * (int64_t)cols > 0 && !mat))
     return fdlp::fail(FDLP_E_INVALID, "fdlp_ark_write: bad args");
-  if (fprintf(w->ark, "%s ", utt) < 0) return fdlp::fail(FDLP_E_IO, "ark write failed");
+  if (fprintf(w->ark, "%s ", utt) < 0) return w->failed = true, fdlp::fail(FDLP_E_IO, "ark write failed");
   const long offset = ftell(w->ark);
   const char hdr[] = {'\0', 'B', 'F', 'M', ' '};
   const char four = 4;
@@ -243,17 +345,29 @@ int fdlp_ark_write(fdlp_ark_writer* w, const char* utt, const float* mat, int32_
   ok &= fwrite(&cols, 4, 1, w->ark) == 1;
   const size_t n = (size_t)rows * (size_t)cols;
   if (n) ok &= fwrite(mat, sizeof(float), n, w->ark) == n;
-  if (!ok) return fdlp::fail(FDLP_E_IO, "ark write failed");
+  if (!ok) return w->failed = true, fdlp::fail(FDLP_E_IO, "ark write failed");
   if (w->scp && fprintf(w->scp, "%s %s:%ld\n", utt, w->ark_abs.c_str(), offset) < 0)
-    return fdlp::fail(FDLP_E_IO, "scp write failed");
+    return w->failed = true, fdlp::fail(FDLP_E_IO, "scp write failed");
   return FDLP_OK;
 }
 
+// Closes the files and renames <ark>.tmp / <scp>.tmp to their final names (a JOB's outputs appear
+// only once complete); after a write failure the temporaries are removed instead.
 int fdlp_ark_close(fdlp_ark_writer* w) {
   if (!w) return FDLP_OK;
   int rc = FDLP_OK;
   if (w->ark && fclose(w->ark) != 0) rc = fdlp::fail(FDLP_E_IO, "ark close failed");
   if (w->scp && fclose(w->scp) != 0) rc = fdlp::fail(FDLP_E_IO, "scp close failed");
+  if (rc != FDLP_OK || w->failed) {
+    remove(w->ark_tmp.c_str());
+    if (w->scp) remove(w->scp_tmp.c_str());
+    if (rc == FDLP_OK) rc = fdlp::fail(FDLP_E_IO, "ark/scp not written (an earlier write failed)");
+  } else {
+    if (rename(w->ark_tmp.c_str(), w->ark_path.c_str()) != 0)
+      rc = fdlp::fail(FDLP_E_IO, "cannot rename " + w->ark_tmp);
+    if (w->scp && rc == FDLP_OK && rename(w->scp_tmp.c_str(), w->scp_path.c_str()) != 0)
+      rc = fdlp::fail(FDLP_E_IO, "cannot rename " + w->scp_tmp);
+  }
   delete w;
   return rc;
 }

@@ -1,0 +1,602 @@
+// fdlp_job.cpp -- native JOB runner behind compute-fdlp-feats: the utterance loop of getFeats
+// (computeFDLPSpectrogram.py:119-237) for one scp shard, with the host work off the Python
+// interpreter:
+//   * reader threads read and parse the scp entries ahead of the consumer, in scp order
+//     (`<path>`, `<cmd> |` through popen, Kaldi `<ark>:<offset>` wave entries; :125-154);
+//   * the consumer applies the reference's per-utterance semantics (skip on read failure, the
+//     sr assertion, noise offsets from the numpy-legacy RNG, :135-166), draws the hop jitter
+//     (CPython-random replica, :225) and packs device batches into pinned buffers;
+//   * each batch is copied in, featurised by fdlp_compute and copied back on one HIP stream, three
+//     batch slots in rotation so the copies, the kernels and the host overlap;
+//   * a writer thread appends the finished utterances to the Kaldi ark/scp (fdlp_ark_*, written to
+//     <name>.tmp and renamed when complete) and the .len lines (:231-237), and the optional global
+//     CMVN stats accumulate on the device (fdlp_cmvn_accumulate).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/fdlp.h"
+#include "fdlp_error.h"
+
+namespace {
+
+using fdlp::fail;
+
+// ---- one scp entry ---------------------------------------------------------------------------
+struct Utt {
+  std::string id;
+  bool ok = false;
+  bool is_int16 = false;
+  int32_t sr = 0, ch = 0;
+  int64_t T = 0;
+  std::vector<int16_t> s16;   // is_int16
+  std::vector<double> f64;    // otherwise (scipy's dtype, converted exactly as numpy does)
+};
+
+bool read_file(const std::string& path, int64_t offset, std::vector<uint8_t>& out) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  bool ok = true;
+  if (offset > 0) ok = fseeko(f, offset, SEEK_SET) == 0;
+  if (ok && offset >= 0 && offset != 0) {  // Kaldi wave archive entry: one RIFF object at the offset
+    uint8_t head[8];
+    ok = fread(head, 1, 8, f) == 8 && !memcmp(head, "RIFF", 4);
+    if (ok) {
+      const uint32_t sz = head[4] | head[5] << 8 | head[6] << 16 | (uint32_t)head[7] << 24;
+      out.assign(head, head + 8);
+      out.resize(8 + (size_t)sz);
+      const size_t got = fread(out.data() + 8, 1, sz, f);
+      out.resize(8 + got);
+    }
+  } else if (ok) {
+    out.clear();
+    uint8_t buf[1 << 16];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof buf, f)) > 0) out.insert(out.end(), buf, buf + n);
+    ok = !ferror(f);
+  }
+  fclose(f);
+  return ok;
+}
+
+bool file_exists(const std::string& p) {
+  FILE* f = fopen(p.c_str(), "rb");
+  if (f) fclose(f);
+  return f != nullptr;
+}
+
+// bytes of the RIFF object an scp entry designates (io_pipeline.read_rx_bytes)
+bool read_rx_bytes(std::string rx, std::vector<uint8_t>& out) {
+  while (!rx.empty() && isspace((unsigned char)rx.back())) rx.pop_back();
+  size_t b = 0;
+  while (b < rx.size() && isspace((unsigned char)rx[b])) ++b;
+  rx = rx.substr(b);
+  if (rx.empty()) return false;
+  if (rx.back() == '|') {  // subprocess.run(cmd, shell=True, stdout=PIPE) (:131-133)
+    FILE* p = popen(rx.substr(0, rx.size() - 1).c_str(), "r");
+    if (!p) return false;
+    out.clear();
+    uint8_t buf[1 << 16];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof buf, p)) > 0) out.insert(out.end(), buf, buf + n);
+    pclose(p);  // the reference ignores the command's exit status too
+    return true;
+  }
+  const size_t colon = rx.find_last_of(':');
+  if (colon != std::string::npos && colon + 1 < rx.size() &&
+      rx.find_first_not_of("0123456789", colon + 1) == std::string::npos && !file_exists(rx) &&
+      file_exists(rx.substr(0, colon)))
+    return read_file(rx.substr(0, colon), strtoll(rx.c_str() + colon + 1, nullptr, 10), out);
+  return read_file(rx, 0, out);
+}
+
+void read_entry(const std::string& line, Utt& u) {
+  // tokens = line.strip().split(); uttid, inwav = tokens[0], ' '.join(tokens[1:])   (:126-127)
+  std::vector<std::string> tok;
+  size_t i = 0;
+  while (i < line.size()) {
+    while (i < line.size() && isspace((unsigned char)line[i])) ++i;
+    size_t j = i;
+    while (j < line.size() && !isspace((unsigned char)line[j])) ++j;
+    if (j > i) tok.push_back(line.substr(i, j - i));
+    i = j;
+  }
+  u.id = tok.empty() ? std::string() : tok[0];
+  std::string rx;
+  for (size_t k = 1; k < tok.size(); ++k) rx += (k > 1 ? " " : "") + tok[k];
+  std::vector<uint8_t> bytes;
+  if (tok.size() < 2 || !read_rx_bytes(rx, bytes)) return;
+  int32_t sr = 0, ch = 0, i16 = 0;
+  int64_t n = 0;
+  if (fdlp_wav_decode(bytes.data(), (int64_t)bytes.size(), &sr, &ch, &i16, &n, nullptr) != FDLP_OK) return;
+  u.sr = sr;
+  u.ch = ch;
+  u.T = n;
+  u.is_int16 = i16 != 0;
+  if (u.is_int16) {
+    int32_t s2, c2;
+    int64_t n2;
+    const int16_t* smp = nullptr;
+    if (fdlp_wav_parse(bytes.data(), (int64_t)bytes.size(), &s2, &c2, &smp, &n2) != FDLP_OK) return;
+    u.s16.resize((size_t)n * ch);
+    memcpy(u.s16.data(), smp, sizeof(int16_t) * u.s16.size());
+  } else {
+    u.f64.resize((size_t)n * ch);
+    if (fdlp_wav_decode(bytes.data(), (int64_t)bytes.size(), nullptr, nullptr, nullptr, nullptr, u.f64.data()) !=
+        FDLP_OK)
+      return;
+  }
+  u.ok = true;
+}
+
+// ---- ordered read-ahead pool -------------------------------------------------------------------
+class Reader {
+ public:
+  Reader(std::vector<std::string> lines, int threads, int depth) : lines_(std::move(lines)), depth_(depth) {
+    slots_.resize(lines_.size());
+    ready_.assign(lines_.size(), 0);
+    for (int t = 0; t < std::max(1, threads); ++t) th_.emplace_back([this] { run(); });
+  }
+  ~Reader() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  size_t size() const { return lines_.size(); }
+  // entry i (blocks until read); the caller releases it with done(i)
+  Utt& get(size_t i) {
+    std::unique_lock<std::mutex> g(m_);
+    cv_done_.wait(g, [&] { return ready_[i] != 0; });
+    return slots_[i];
+  }
+  void done(size_t i) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      slots_[i] = Utt();
+      consumed_ = i + 1;
+    }
+    cv_.notify_all();
+  }
+
+ private:
+  void run() {
+    for (;;) {
+      size_t i;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || (next_ < lines_.size() && next_ < consumed_ + depth_); });
+        if (stop_ || next_ >= lines_.size()) return;
+        i = next_++;
+      }
+      Utt u;
+      read_entry(lines_[i], u);
+      {
+        std::lock_guard<std::mutex> g(m_);
+        slots_[i] = std::move(u);
+        ready_[i] = 1;
+      }
+      cv_done_.notify_all();
+    }
+  }
+  std::vector<std::string> lines_;
+  std::vector<Utt> slots_;
+  std::vector<char> ready_;
+  size_t next_ = 0, consumed_ = 0, depth_;
+  bool stop_ = false;
+  std::mutex m_;
+  std::condition_variable cv_, cv_done_;
+  std::vector<std::thread> th_;
+};
+
+// ---- writer thread ----------------------------------------------------------------------------
+struct Done {
+  int slot;
+  std::vector<std::string> ids;
+  std::vector<int64_t> rows;  // n + 1 row offsets into the slot's host output
+};
+
+struct Slot {
+  int kind = FDLP_PCM_I16;
+  void* h_pcm = nullptr;       // pinned
+  size_t pcm_cap = 0;          // bytes
+  void* d_pcm = nullptr;
+  size_t d_pcm_cap = 0;
+  float* h_out = nullptr;      // pinned
+  float* d_out = nullptr;
+  size_t out_cap = 0;          // floats
+  hipEvent_t done = nullptr;
+  bool busy = false;           // in flight or not yet written
+};
+
+struct JobState {
+  std::mutex m;
+  std::condition_variable cv;
+  std::deque<Done> queue;
+  bool finish = false;
+  int err = FDLP_OK;
+  std::string err_msg;
+  std::vector<Slot>* slots = nullptr;
+};
+
+int grow_pinned(void** p, size_t* cap, size_t need) {
+  if (*cap >= need) return FDLP_OK;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  const size_t n = std::max(need, *cap * 3 / 2);
+  if (hipHostMalloc(p, n, hipHostMallocDefault) != hipSuccess) return fail(FDLP_E_NOMEM, "pinned host allocation failed");
+  *cap = n;
+  return FDLP_OK;
+}
+
+int grow_device(void** p, size_t* cap, size_t need, hipStream_t s) {
+  if (*cap >= need) return FDLP_OK;
+  if (*p) {
+    if (hipStreamSynchronize(s) != hipSuccess) return fail(FDLP_E_HIP, "stream sync failed");
+    (void)hipFree(*p);
+  }
+  *p = nullptr;
+  const size_t n = std::max(need, *cap * 3 / 2);
+  if (hipMalloc(p, n) != hipSuccess) return fail(FDLP_E_NOMEM, "device allocation failed");
+  *cap = n;
+  return FDLP_OK;
+}
+
+}  // namespace
+
+extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_path, const char* outfile,
+                            const fdlp_job_opts* o, fdlp_job_stats* st) {
+  if (!cfg || !scp_path || !outfile || !o) return fail(FDLP_E_INVALID, "fdlp_job_run: null argument");
+  if (o->scp_type != 0 && o->scp_type != 1) return fail(FDLP_E_INVALID, "Invalid type of scp type, it should be either wav or segment");
+  if (cfg->mode != FDLP_MODE_SPECTROGRAM) return fail(FDLP_E_INVALID, "fdlp_job_run: spectrogram plans only");
+  if (o->noise && o->preprocess == FDLP_PRE_DIFF) return fail(FDLP_E_INVALID, "fdlp_job_run: diff and noise are exclusive");
+  struct timespec t0;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  fdlp_job_stats stats{};
+
+  // scp lines (for line in fid: every line, blank lines included, is an entry of the reference; a
+  // blank line raises IndexError there; here blank lines are ignored like the Python drop-in)
+  std::vector<std::string> lines;
+  {
+    FILE* f = fopen(scp_path, "r");
+    if (!f) return fail(FDLP_E_IO, std::string("cannot open scp ") + scp_path);
+    std::string cur;
+    int c;
+    while ((c = fgetc(f)) != EOF) {
+      if (c == '\n') {
+        if (cur.find_first_not_of(" \t\r") != std::string::npos) lines.push_back(cur);
+        cur.clear();
+      } else {
+        cur.push_back((char)c);
+      }
+    }
+    if (cur.find_first_not_of(" \t\r") != std::string::npos) lines.push_back(cur);
+    fclose(f);
+  }
+  stats.n_lines = (int64_t)lines.size();
+
+  fdlp_config c = *cfg;
+  c.max_frames = std::max(1, o->batch_frames);
+  fdlp_plan* plan = nullptr;
+  int rc = fdlp_plan_create(&c, device, &plan);
+  if (rc != FDLP_OK) return rc;
+  int32_t B = 0;
+  fdlp_plan_out_dim(plan, &B);
+
+  int prev_dev = -1;
+  (void)hipGetDevice(&prev_dev);
+  hipStream_t s = nullptr;
+  fdlp_pyrandom* jrng = nullptr;
+  fdlp_nprandom* nrng = nullptr;
+  fdlp_ark_writer* ark = nullptr;
+  int16_t* d_noise = nullptr;
+  double* d_cmvn = nullptr;
+  std::vector<Slot> slots(3);
+  JobState js;
+  js.slots = &slots;
+  std::string len_text;
+  std::thread writer;
+  int32_t sr_seen = -1;  // 'sr' of the last successful read (:139; NameError before the first one)
+
+  auto cleanup = [&](int code) -> int {
+    std::string keep = code != FDLP_OK ? fdlp::last_error_slot() : std::string();
+    if (writer.joinable()) {
+      {
+        std::lock_guard<std::mutex> g(js.m);
+        js.finish = true;
+      }
+      js.cv.notify_all();
+      writer.join();
+    }
+    if (s) (void)hipStreamSynchronize(s);
+    for (auto& sl : slots) {
+      if (sl.h_pcm) (void)hipHostFree(sl.h_pcm);
+      if (sl.h_out) (void)hipHostFree(sl.h_out);
+      if (sl.d_pcm) (void)hipFree(sl.d_pcm);
+      if (sl.d_out) (void)hipFree(sl.d_out);
+      if (sl.done) (void)hipEventDestroy(sl.done);
+    }
+    if (d_noise) (void)hipFree(d_noise);
+    if (d_cmvn) (void)hipFree(d_cmvn);
+    if (s) (void)hipStreamDestroy(s);
+    if (jrng) fdlp_pyrandom_destroy(jrng);
+    if (nrng) fdlp_nprandom_destroy(nrng);
+    if (ark) {
+      const int rc2 = fdlp_ark_close(ark);
+      if (code == FDLP_OK && rc2 != FDLP_OK) {
+        code = rc2;
+        keep = fdlp::last_error_slot();
+      }
+    }
+    fdlp_plan_destroy(plan);
+    if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
+    struct timespec t1;
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    stats.seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    if (st) *st = stats;
+    if (code != FDLP_OK) fdlp::last_error_slot() = keep;
+    return code;
+  };
+#define JOB_TRY(expr) do { int rc_ = (expr); if (rc_ != FDLP_OK) return cleanup(rc_); } while (0)
+#define JOB_HIP(expr) do { hipError_t e_ = (expr); if (e_ != hipSuccess) return cleanup(fail(FDLP_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_))); } while (0)
+
+  JOB_HIP(hipSetDevice(device));
+  JOB_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  for (auto& sl : slots) JOB_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  JOB_TRY(fdlp_pyrandom_create(o->jitter_key, o->jitter_key_len, &jrng));
+  if (o->noise) {
+    JOB_TRY(fdlp_nprandom_create(o->noise_seed, &nrng));
+    JOB_HIP(hipMalloc((void**)&d_noise, sizeof(int16_t) * std::max<int64_t>(o->noise_len, 1)));
+    JOB_HIP(hipMemcpy(d_noise, o->noise, sizeof(int16_t) * o->noise_len, hipMemcpyHostToDevice));
+  }
+  if (o->cmvn_path) {
+    JOB_HIP(hipMalloc((void**)&d_cmvn, sizeof(double) * 2 * (B + 1)));
+    JOB_HIP(hipMemsetAsync(d_cmvn, 0, sizeof(double) * 2 * (B + 1), s));
+  }
+  const std::string out_s(outfile);
+  JOB_TRY(fdlp_ark_open((out_s + ".ark").c_str(), (out_s + ".scp").c_str(), &ark));
+
+  // writer: ark/scp + .len of finished batches, in order
+  writer = std::thread([&] {
+    for (;;) {
+      Done d;
+      {
+        std::unique_lock<std::mutex> g(js.m);
+        js.cv.wait(g, [&] { return js.finish || !js.queue.empty(); });
+        if (js.queue.empty()) return;
+        d = std::move(js.queue.front());
+        js.queue.pop_front();
+      }
+      Slot& sl = slots[d.slot];
+      int err = FDLP_OK;
+      std::string msg;
+      if (hipEventSynchronize(sl.done) != hipSuccess) {
+        err = FDLP_E_HIP;
+        msg = "device batch failed";
+      }
+      for (size_t i = 0; i < d.ids.size() && err == FDLP_OK; ++i) {
+        const int64_t r0 = d.rows[i], r1 = d.rows[i + 1];
+        if (fdlp_ark_write(ark, d.ids[i].c_str(), sl.h_out + r0 * B, (int32_t)(r1 - r0), B) != FDLP_OK) {
+          err = FDLP_E_IO;
+          msg = fdlp::last_error_slot();
+        }
+        if (o->write_len) len_text += d.ids[i] + " " + std::to_string(r1 - r0) + "\n";  // :235-236
+      }
+      {
+        std::lock_guard<std::mutex> g(js.m);
+        sl.busy = false;
+        if (err != FDLP_OK && js.err == FDLP_OK) {
+          js.err = err;
+          js.err_msg = msg;
+        }
+      }
+      js.cv.notify_all();
+    }
+  });
+
+  Reader reader(lines, std::max(1, o->io_threads), 64);
+  const size_t pcm_elem_i16 = sizeof(int16_t), pcm_elem_f64 = sizeof(double);
+  struct Pending {
+    std::vector<std::string> ids;
+    std::vector<int64_t> off, len, noff, rows;
+    std::vector<double> alpha;
+    std::vector<uint8_t> jit;
+    int64_t frames = 0, samples = 0, out_rows = 0;
+    int kind = FDLP_PCM_I16;
+  } pend;
+  int slot_i = 0;
+
+  // waits until the slot's previous batch is written, then makes it the current one
+  auto acquire_slot = [&](int k) -> int {
+    std::unique_lock<std::mutex> g(js.m);
+    js.cv.wait(g, [&] { return !slots[k].busy || js.err != FDLP_OK; });
+    if (js.err != FDLP_OK) return fail(js.err, js.err_msg);
+    return FDLP_OK;
+  };
+  JOB_TRY(acquire_slot(slot_i));
+
+  auto flush = [&]() -> int {
+    if (pend.ids.empty()) return FDLP_OK;
+    Slot& sl = slots[slot_i];
+    const size_t elem = pend.kind == FDLP_PCM_I16 ? pcm_elem_i16 : pcm_elem_f64;
+    int r = grow_device(&sl.d_pcm, &sl.d_pcm_cap, (size_t)pend.samples * elem, s);
+    if (r != FDLP_OK) return r;
+    r = grow_device((void**)&sl.d_out, &sl.out_cap, sizeof(float) * (size_t)pend.out_rows * B, s);
+    if (r != FDLP_OK) return r;
+    if (hipMemcpyAsync(sl.d_pcm, sl.h_pcm, (size_t)pend.samples * elem, hipMemcpyHostToDevice, s) != hipSuccess)
+      return fail(FDLP_E_HIP, "H2D copy failed");
+    fdlp_batch b{};
+    b.n_utt = (int32_t)pend.ids.size();
+    b.pcm_kind = pend.kind;
+    b.pcm_dev = sl.d_pcm;
+    b.pcm_off = pend.off.data();
+    b.utt_len = pend.len.data();
+    b.jitter = pend.jit.empty() ? nullptr : pend.jit.data();
+    b.noise_dev = o->noise ? d_noise : nullptr;
+    b.noise_off = o->noise ? pend.noff.data() : nullptr;
+    b.noise_alpha = o->noise ? pend.alpha.data() : nullptr;
+    b.out_dev = sl.d_out;
+    b.out_row = pend.rows.data();
+    b.out_f64_dev = nullptr;
+    b.ark_decimals = o->ark_decimals;
+    b.preprocess = o->preprocess;
+    r = fdlp_compute(plan, &b, s);
+    if (r != FDLP_OK) return r;
+    if (d_cmvn) {
+      r = fdlp_cmvn_accumulate(sl.d_out, pend.out_rows, B, d_cmvn, s);
+      if (r != FDLP_OK) return r;
+    }
+    if (hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * (size_t)pend.out_rows * B, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipEventRecord(sl.done, s) != hipSuccess)
+      return fail(FDLP_E_HIP, "D2H copy failed");
+    Done d;
+    d.slot = slot_i;
+    d.ids = std::move(pend.ids);
+    d.rows = std::move(pend.rows);
+    d.rows.push_back(pend.out_rows);
+    {
+      std::lock_guard<std::mutex> g(js.m);
+      sl.busy = true;
+      js.queue.push_back(std::move(d));
+    }
+    js.cv.notify_all();
+    if (o->progress_name) fflush(stdout);
+    pend = Pending();
+    slot_i = (slot_i + 1) % (int)slots.size();
+    return acquire_slot(slot_i);
+  };
+
+  std::vector<size_t> hout_cap(slots.size(), 0);  // bytes of each slot's pinned output
+
+  for (size_t i = 0; i < reader.size(); ++i) {
+    Utt& u = reader.get(i);
+    const bool skip = !u.ok;
+    if (!skip) sr_seen = u.sr;
+    if (o->scp_type == 0) {
+      if (sr_seen < 0) return cleanup(fail(FDLP_E_INVALID, "name 'sr' is not defined"));  // :144 before any read
+      if (sr_seen != o->srate) return cleanup(fail(FDLP_E_INVALID, "Input file has different sampling rate."));
+    }
+    if (skip) {
+      ++stats.n_skipped;
+      reader.done(i);
+      continue;
+    }
+    if (u.ch != 1) return cleanup(fail(FDLP_E_INVALID, "multi-channel WAV input is not supported (the reference expects mono)"));
+    const int64_t T = u.T;
+    int32_t F = 0, L = 0;
+    fdlp_geometry(plan, T, &F, &L);
+    if (F < 1) return cleanup(fail(FDLP_E_INVALID, "invalid number of data points (0) specified"));
+    const int kind = u.is_int16 ? FDLP_PCM_I16 : FDLP_PCM_F64;
+    if ((o->noise || o->preprocess == FDLP_PRE_DIFF) && kind != FDLP_PCM_I16)
+      return cleanup(fail(FDLP_E_INVALID, "noise mixing / diff preprocessing need 16-bit PCM input"));
+    int64_t noff = 0;
+    double alpha = 0.0;
+    if (o->noise) {  // add_noise_to_wav (features.py:24-31), np.random.rand() per utterance (:166)
+      double uu = 0.0;
+      JOB_TRY(fdlp_nprandom_rand(nrng, 1, &uu));
+      JOB_TRY(fdlp_noise_params(u.s16.data(), T, o->noise, o->noise_len, o->snr, uu, &noff, &alpha));
+    }
+    if (o->progress_name) printf("%s: Computing Features for file: %s\n", o->progress_name, u.id.c_str());  // :185
+    // a batch is one PCM kind and at most max_frames frames
+    int32_t cap = c.max_frames;
+    if (!pend.ids.empty() && (pend.frames + F > cap || pend.kind != kind)) JOB_TRY(flush());
+    if (F > cap) {  // an utterance longer than a batch: a bigger plan (the Python drop-in does the same)
+      JOB_HIP(hipStreamSynchronize(s));
+      {
+        std::unique_lock<std::mutex> g(js.m);
+        js.cv.wait(g, [&] { return js.queue.empty() || js.err != FDLP_OK; });
+      }
+      fdlp_plan_destroy(plan);
+      plan = nullptr;
+      c.max_frames = F;
+      JOB_TRY(fdlp_plan_create(&c, device, &plan));
+      cap = F;
+    }
+    // append to the current slot's pinned PCM
+    Slot& sl = slots[slot_i];
+    const size_t elem = kind == FDLP_PCM_I16 ? pcm_elem_i16 : pcm_elem_f64;
+    const size_t need = (size_t)(pend.samples + T) * elem;
+    if (need > sl.pcm_cap) {
+      std::vector<uint8_t> keep((size_t)pend.samples * elem);
+      if (pend.samples) memcpy(keep.data(), sl.h_pcm, keep.size());
+      JOB_TRY(grow_pinned(&sl.h_pcm, &sl.pcm_cap, std::max(need, (size_t)c.max_frames * 18000 * elem)));
+      if (!keep.empty()) memcpy(sl.h_pcm, keep.data(), keep.size());
+    }
+    if (kind == FDLP_PCM_I16) memcpy((int16_t*)sl.h_pcm + pend.samples, u.s16.data(), sizeof(int16_t) * T);
+    else memcpy((double*)sl.h_pcm + pend.samples, u.f64.data(), sizeof(double) * T);
+    // pinned host output for this batch's rows
+    const size_t rows_need = (size_t)(pend.out_rows + L);
+    if (rows_need * B * sizeof(float) > hout_cap[slot_i]) {
+      const size_t nb = std::max(rows_need * B * sizeof(float), (size_t)c.max_frames * 120 * B * sizeof(float));
+      if (sl.h_out) (void)hipHostFree(sl.h_out);
+      sl.h_out = nullptr;
+      JOB_HIP(hipHostMalloc((void**)&sl.h_out, nb, hipHostMallocDefault));
+      hout_cap[slot_i] = nb;
+    }
+    pend.kind = kind;
+    pend.ids.push_back(u.id);
+    pend.off.push_back(pend.samples);
+    pend.len.push_back(T);
+    pend.noff.push_back(noff);
+    pend.alpha.push_back(alpha);
+    pend.rows.push_back(pend.out_rows);
+    const size_t j0 = pend.jit.size();
+    pend.jit.resize(j0 + (size_t)(F - 1));
+    if (F > 1) JOB_TRY(fdlp_pyrandom_randbits2(jrng, F - 1, pend.jit.data() + j0));  // randrange(2) (:225)
+    pend.frames += F;
+    pend.samples += T;
+    pend.out_rows += L;
+    ++stats.n_done;
+    stats.n_samples += T;
+    stats.n_frames_out += L;
+    reader.done(i);
+  }
+  JOB_TRY(flush());
+  {
+    std::unique_lock<std::mutex> g(js.m);
+    js.cv.wait(g, [&] { return js.queue.empty() || js.err != FDLP_OK; });
+    if (js.err != FDLP_OK) return cleanup(fail(js.err, js.err_msg));
+  }
+  JOB_HIP(hipStreamSynchronize(s));
+  {  // wait for the writer to finish the last batches
+    std::unique_lock<std::mutex> g(js.m);
+    js.cv.wait(g, [&] {
+      for (auto& sl : slots)
+        if (sl.busy) return js.err != FDLP_OK;
+      return true;
+    });
+    if (js.err != FDLP_OK) return cleanup(fail(js.err, js.err_msg));
+  }
+  if (o->write_len) {  // <outfile>.len (:232-237), written whole then renamed
+    const std::string tmp = out_s + ".len.tmp";
+    FILE* f = fopen(tmp.c_str(), "w");
+    if (!f) return cleanup(fail(FDLP_E_IO, "cannot open " + tmp));
+    const bool ok = fwrite(len_text.data(), 1, len_text.size(), f) == len_text.size();
+    if (fclose(f) != 0 || !ok || rename(tmp.c_str(), (out_s + ".len").c_str()) != 0) {
+      remove(tmp.c_str());
+      return cleanup(fail(FDLP_E_IO, "cannot write " + out_s + ".len"));
+    }
+  }
+  if (d_cmvn) {
+    std::vector<double> h(2 * (size_t)(B + 1));
+    JOB_HIP(hipMemcpy(h.data(), d_cmvn, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
+    JOB_TRY(fdlp_kaldi_write_dmatrix(o->cmvn_path, h.data(), 2, B + 1, 1));
+  }
+#undef JOB_TRY
+#undef JOB_HIP
+  return cleanup(FDLP_OK);
+}

@@ -64,6 +64,10 @@ def build_parser():
     parser.add_argument('--cmvn_stats', type=str, default=None,
                         help='also write the global CMVN stats of the written features (Kaldi compute-cmvn-stats '
                              'format, accumulated on the device) to this file')
+    parser.add_argument('--host_runner', choices=('native', 'python'), default='native',
+                        help='native: the C++ JOB runner of libfdlp_hip.so (fdlp_job_run: reader threads, '
+                             'pinned double-buffered batches, writer thread); python: the same loop in Python '
+                             '(always used with --add_reverb)')
     return parser
 
 
@@ -112,6 +116,8 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
         raise ValueError('Invalid type of scp type, it should be either wav or segment')
 
     device = args.device if args.device is not None else int(os.environ.get("LOCAL_RANK", "0"))
+    if getattr(args, 'host_runner', 'python') == 'native' and rir is None and not return_feats:
+        return _run_native(args, cfg, device, noise, snr if noise is not None else 0.0, diff)
     torch.cuda.set_device(device)
     plan = FdlpPlan(cfg, device=device, max_frames=max(int(args.batch_frames), 1))
     jit_rng = PyRandom(args.seed)
@@ -177,9 +183,11 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
             complete(inflight.popleft())
 
     sr = None
+    n_lines = n_skipped = 0
     workers = max(1, int(getattr(args, 'io_workers', 4) or 1))
     try:
         for uttid, sig, sr_new in PrefetchReader(wavs, scp_type, workers=workers):   # :125
+            n_lines += 1
             skip = sig is None
             if not skip:
                 sr = sr_new
@@ -188,9 +196,14 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
                     raise NameError("name 'sr' is not defined")
                 assert sr == srate, 'Input file has different sampling rate.'  # :144
             if skip:
+                n_skipped += 1
                 continue
             if sig.ndim != 1:
                 raise ValueError("multi-channel WAV input is not supported (the reference expects mono)")
+            if sig.dtype != np.int16 and (noise is not None or diff):
+                raise NotImplementedError("noise mixing / diff preprocessing need 16-bit PCM input")
+            if pending and pending[-1][1].dtype != sig.dtype:
+                flush()  # a device batch holds one sample type (int16 or the float64 of other formats)
             T = sig.shape[0]
             F, _ = plan.geometry(T)
             if F < 1:
@@ -215,14 +228,79 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
     finally:
         ark.close()
     if args.write_utt2num_frames:                                           # :232-237
-        with open(outfile + '.len', 'w+') as file:
+        with open(outfile + '.len.tmp', 'w+') as file:
             for key, lens in all_lens.items():
                 file.write("{:s} {:d}".format(key, lens))
                 file.write("\n")
+        os.replace(outfile + '.len.tmp', outfile + '.len')
     if cmvn is not None:
         from speech_recognition_tools_amd.cmvn import write_kaldi_dmatrix
         write_kaldi_dmatrix(args.cmvn_stats, cmvn.numpy(), binary=True)
+    _report_skips(n_lines, n_skipped)
     return all_feats
+
+
+def _report_skips(n_lines, n_skipped):
+    """The reference skips unreadable entries silently (:135-142); here they are counted and reported,
+    and a JOB in which every entry was skipped fails."""
+    if n_skipped:
+        print('%s: skipped %d of %d utterances (unreadable)' % (sys.argv[0], n_skipped, n_lines))
+        sys.stdout.flush()
+    if n_lines and n_skipped == n_lines:
+        raise RuntimeError('every utterance of the scp was skipped (unreadable)')
+
+
+def _seed_words(seed, n_random=624):
+    """CPython random.seed key words (rng._int_key), or OS entropy like an unseeded random."""
+    from speech_recognition_tools_amd.rng import _int_key
+    if seed is None:
+        return np.frombuffer(os.urandom(n_random * 4), dtype=np.uint32).copy()
+    return np.asarray(_int_key(seed), dtype=np.uint32)
+
+
+def _run_native(args, cfg, device, noise, snr, diff):
+    """The JOB loop in libfdlp_hip.so (fdlp_job_run): reader threads, pinned batches with the copies and
+    kernels of consecutive batches overlapped, writer thread; same outputs and semantics as the Python loop."""
+    import ctypes
+    from speech_recognition_tools_amd import _lib
+    c, keep = cfg.to_c(max(int(args.batch_frames), 1))
+    o = _lib.FdlpJobOptsC()
+    o.scp_type = 0 if args.scp_type == 'wav' else 1
+    o.write_len = int(bool(args.write_utt2num_frames))
+    o.ark_decimals = int(args.ark_precision)
+    o.batch_frames = max(int(args.batch_frames), 1)
+    o.io_threads = max(1, int(getattr(args, 'io_workers', 4) or 1))
+    o.preprocess = _lib.FDLP_PRE_DIFF if diff else _lib.FDLP_PRE_NONE
+    hold = []
+    if noise is not None:
+        nz = np.ascontiguousarray(noise, dtype=np.int16)
+        hold.append(nz)
+        o.noise, o.noise_len, o.snr = _lib.ptr(nz, ctypes.c_int16), nz.size, float(snr)
+        seed = args.noise_seed
+        if seed is None:
+            seed = int(np.frombuffer(os.urandom(4), dtype=np.uint32)[0])
+        if not 0 <= int(seed) <= 0xFFFFFFFF:
+            raise ValueError("Seed must be between 0 and 2**32 - 1")
+        o.noise_seed = int(seed)
+    key = _seed_words(args.seed)
+    hold.append(key)
+    o.jitter_key, o.jitter_key_len = _lib.ptr(key, ctypes.c_uint32), key.size
+    o.srate = 16000
+    o.progress_name = sys.argv[0].encode()
+    o.cmvn_path = args.cmvn_stats.encode() if args.cmvn_stats else None
+    st = _lib.FdlpJobStatsC()
+    sys.stdout.flush()
+    rc = _lib.lib.fdlp_job_run(ctypes.byref(c), int(device), args.scp.encode(), args.outfile.encode(),
+                               ctypes.byref(o), ctypes.byref(st))
+    if rc != _lib.FDLP_OK:
+        msg = _lib.lib.fdlp_last_error().decode("utf-8", "replace")
+        if msg == "name 'sr' is not defined":
+            raise NameError(msg)                                            # :144 before any read
+        if msg == 'Input file has different sampling rate.':
+            raise AssertionError(msg)                                       # :144
+        _lib.check(rc)
+    _report_skips(st.n_lines, st.n_skipped)
+    return None
 
 
 def main(argv=None):

@@ -20,14 +20,25 @@ from .._lib import FdlpConfigC, FDLP_FBANK_COCHLEAR, FDLP_FBANK_MEL, check, lib,
 
 
 def read_wav_bytes(data: bytes):
-    """(sr, int16 samples) of a RIFF/WAVE PCM16 buffer (replaces scipy.io.wavfile.read)."""
+    """(sr, samples) of a RIFF/WAVE buffer like scipy.io.wavfile.read (computeFDLPSpectrogram.py:133,:139):
+    int16 for 16-bit PCM; the other formats scipy reads (8-bit unsigned, 24/32/64-bit integer, float32/64)
+    come back as the float64 values of scipy's array (the reference only ever multiplies them by a float64
+    window, features.py:153).  Multi-channel data is [T, channels]."""
     buf = np.frombuffer(data, dtype=np.uint8)
-    sr, ch, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
-    sp = ctypes.POINTER(ctypes.c_int16)()
-    check(lib.fdlp_wav_parse(ptr(buf, ctypes.c_uint8), buf.size, ctypes.byref(sr), ctypes.byref(ch),
-                             ctypes.byref(sp), ctypes.byref(n)))
-    off = ctypes.cast(sp, ctypes.c_void_p).value - buf.ctypes.data
-    x = np.frombuffer(data, dtype='<i2', count=n.value * ch.value, offset=off).astype(np.int16)
+    sr, ch, i16, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+    check(lib.fdlp_wav_decode(ptr(buf, ctypes.c_uint8), buf.size, ctypes.byref(sr), ctypes.byref(ch),
+                              ctypes.byref(i16), ctypes.byref(n), None))
+    if i16.value:
+        sp = ctypes.POINTER(ctypes.c_int16)()
+        sr2, ch2, n2 = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        check(lib.fdlp_wav_parse(ptr(buf, ctypes.c_uint8), buf.size, ctypes.byref(sr2), ctypes.byref(ch2),
+                                 ctypes.byref(sp), ctypes.byref(n2)))
+        off = ctypes.cast(sp, ctypes.c_void_p).value - buf.ctypes.data
+        x = np.frombuffer(data, dtype='<i2', count=n.value * ch.value, offset=off).astype(np.int16)
+    else:
+        x = np.empty(n.value * ch.value, dtype=np.float64)
+        check(lib.fdlp_wav_decode(ptr(buf, ctypes.c_uint8), buf.size, None, None, None, None,
+                                  ptr(x, ctypes.c_double)))
     if ch.value > 1:
         x = x.reshape(-1, ch.value)
     return sr.value, x

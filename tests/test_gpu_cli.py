@@ -17,6 +17,16 @@ def _args(extra):
     return build_parser().parse_args(extra)
 
 
+def _run(extra, runner):
+    """The CLI's getFeats (no feature dict returned) through the native JOB runner (fdlp_job_run) or the
+    Python loop."""
+    from speech_recognition_tools_amd.featgen.computeFDLPSpectrogram import getFeats
+    getFeats(_args(extra + ["--host_runner=" + runner]), return_feats=False)
+
+
+RUNNERS = pytest.mark.parametrize("runner", ["native", "python"])
+
+
 def _write_scp(tmp, sig, utts, pipe=()):
     scp = os.path.join(tmp, "wav.scp")
     with open(scp, "w") as f:
@@ -50,50 +60,155 @@ def _check(out, meta, ref, utts):
         assert line.split()[0] in utts
 
 
-def test_cli_wsj_files_and_pipes(tmp_path):
+def test_cli_wsj_files_and_pipes_return_feats(tmp_path):
+    """getFeats returning the feature dict (the Python loop) equals the ark it writes."""
     from speech_recognition_tools_amd.featgen.computeFDLPSpectrogram import getFeats
+    from speech_recognition_tools_amd.featgen.features import read_ark
     meta, sig, ref, z = load_golden("wsj")
     utts = meta["utts"]
     scp = _write_scp(str(tmp_path), sig, utts, pipe=("s4p0", "white10"))
     out = str(tmp_path / "melspec_test.1")
-    getFeats(_args([scp, out] + _opts(meta) + ["--batch_frames=16"]))
+    feats = getFeats(_args([scp, out] + _opts(meta) + ["--batch_frames=16"]))
     _check(out, meta, ref, utts)
+    ark = read_ark(out + ".ark")
+    for u in utts:
+        np.testing.assert_array_equal(feats[u], ark[u])
 
 
-def test_cli_skips_unreadable_utterances(tmp_path):
-    from speech_recognition_tools_amd.featgen.computeFDLPSpectrogram import getFeats
+@RUNNERS
+def test_cli_wsj_files_and_pipes(tmp_path, runner):
+    meta, sig, ref, z = load_golden("wsj")
+    utts = meta["utts"]
+    scp = _write_scp(str(tmp_path), sig, utts, pipe=("s4p0", "white10"))
+    out = str(tmp_path / "melspec_test.1")
+    _run([scp, out] + _opts(meta) + ["--batch_frames=16"], runner)
+    _check(out, meta, ref, utts)
+    assert not any(f.endswith(".tmp") for f in os.listdir(str(tmp_path)))  # renamed when complete
+
+
+@RUNNERS
+def test_cli_skips_unreadable_utterances(tmp_path, runner, capfd):
     meta, sig, ref, z = load_golden("reverb")
     utts = meta["utts"]
     scp = _write_scp(str(tmp_path), sig, utts)
     with open(scp, "a") as f:
         f.write("missing_utt %s\n" % str(tmp_path / "nope.wav"))
+        f.write("garbage_utt %s\n" % scp)  # not a WAV
     out = str(tmp_path / "o")
-    getFeats(_args([scp, out] + _opts(meta)))
+    _run([scp, out] + _opts(meta), runner)
     _check(out, meta, ref, utts)
+    assert "skipped 2 of %d utterances" % (len(utts) + 2) in capfd.readouterr().out
     # a failing FIRST utterance leaves the reference's `sr` undefined -> NameError (:144)
     bad = str(tmp_path / "bad.scp")
     with open(bad, "w") as f:
         f.write("missing_utt %s\n" % str(tmp_path / "nope.wav"))
     with pytest.raises(NameError):
-        getFeats(_args([bad, out] + _opts(meta)))
+        _run([bad, out] + _opts(meta), runner)
+    # every entry of a segment scp unreadable: the JOB fails (the reference would write nothing)
+    with pytest.raises(RuntimeError, match="every utterance"):
+        _run([bad, str(tmp_path / "seg")] + _opts(meta) + ["--scp_type=segment"], runner)
 
 
-def test_cli_rejects_other_sample_rates(tmp_path):
-    from speech_recognition_tools_amd.featgen.computeFDLPSpectrogram import getFeats
+@RUNNERS
+def test_cli_rejects_other_sample_rates(tmp_path, runner):
     p = str(tmp_path / "a.wav")
     wavfile.write(p, 8000, np.zeros(16000, dtype=np.int16))
     scp = str(tmp_path / "w.scp")
     open(scp, "w").write("u %s\n" % p)
     with pytest.raises(AssertionError, match="different sampling rate"):
-        getFeats(_args([scp, str(tmp_path / "o")]))
+        _run([scp, str(tmp_path / "o")], runner)
 
 
-def test_cli_diff_and_noise(tmp_path, monkeypatch):
-    from speech_recognition_tools_amd.featgen.computeFDLPSpectrogram import getFeats
+def _write_formats(tmp, x):
+    """The int16 signal x in the WAV formats scipy reads, and the values scipy returns for each."""
+    import struct
+    files = {}
+    p = os.path.join(tmp, "f32.wav")
+    wavfile.write(p, 16000, (x / 32768.0).astype(np.float32))
+    files["f32"] = p
+    p = os.path.join(tmp, "f64.wav")
+    wavfile.write(p, 16000, x.astype(np.float64) * 0.5)
+    files["f64"] = p
+    p = os.path.join(tmp, "i32.wav")
+    wavfile.write(p, 16000, x.astype(np.int32) * 65536)
+    files["i32"] = p
+    p = os.path.join(tmp, "u8.wav")
+    wavfile.write(p, 16000, (x // 256 + 128).astype(np.uint8))
+    files["u8"] = p
+    # 24-bit PCM (scipy returns it left-justified in int32)
+    v = x.astype(np.int32) * 256 + 17
+    raw = b"".join(struct.pack("<i", int(s))[:3] for s in v)
+    hdr = (b"RIFF" + struct.pack("<I", 36 + len(raw)) + b"WAVEfmt " + struct.pack("<IHHIIHH", 16, 1, 1, 16000,
+           16000 * 3, 3, 24) + b"data" + struct.pack("<I", len(raw)))
+    p = os.path.join(tmp, "i24.wav")
+    open(p, "wb").write(hdr + raw)
+    files["i24"] = p
+    return files
+
+
+@RUNNERS
+def test_cli_scipy_wav_formats(tmp_path, runner):
+    """Every format scipy.io.wavfile.read returns (the reference featurises its values as they are, no
+    scaling, :156-157) gives the oracle's features of scipy's values; int16 and other-format utterances
+    in one scp go to separate device batches."""
+    import random
+    from scipy.io.wavfile import read
+    from oracle import fdlp_oracle as O
+    from speech_recognition_tools_amd.featgen.features import read_ark
+    rng = np.random.default_rng(11)
+    x = np.clip(rng.standard_normal(30000) * 3000, -32768, 32767).astype(np.int16)
+    files = _write_formats(str(tmp_path), x)
+    p16 = str(tmp_path / "i16.wav")
+    wavfile.write(p16, 16000, x)
+    order = ["f32", "i16", "i24", "u8", "f64", "i32"]
+    files["i16"] = p16
+    scp = str(tmp_path / "w.scp")
+    with open(scp, "w") as f:
+        for k in order:
+            f.write("%s %s\n" % (k, files[k]))
+    out = str(tmp_path / "fmt")
+    cfg = O.FdlpConfig.wsj()
+    opts = ["--nfilters=80", "--coeff_num=100", "--coeff_range=0,100", "--order=150", "--fduration=1.5",
+            "--frate=100", "--overlap_fraction=0.25", "--fbank_type=cochlear,1,1,1,2.5,1", "--seed=4",
+            "--ark_precision=-1"]
+    _run([scp, out] + opts, runner)
+    ark = read_ark(out + ".ark")
+    assert list(ark) == order
+    orc = O.FdlpOracle(cfg)
+    r = random.Random(4)
+    for k in order:
+        sr, v = read(files[k])
+        want = orc.utterance(v.astype(np.float64) if v.dtype != np.int16 else v, r)
+        assert np.abs(ark[k] - want.astype(np.float32)).max() <= 1e-4 * max(1.0, np.abs(want).max()), k
+
+
+def test_native_and_python_runners_write_identical_arks(tmp_path):
+    """Same scp (files, a pipe, an unreadable entry, a long utterance that outgrows the batch) through
+    both host runners: byte-identical .ark / .len and identical scp keys and offsets."""
+    meta, sig, ref, z = load_golden("wsj")
+    utts = meta["utts"]
+    scp = _write_scp(str(tmp_path), sig, utts, pipe=("s4p0",))
+    with open(scp, "a") as f:
+        f.write("missing_utt %s\n" % str(tmp_path / "nope.wav"))
+    outs = {}
+    for runner in ("native", "python"):
+        out = str(tmp_path / runner)
+        _run([scp, out] + _opts(meta) + ["--batch_frames=8"], runner)
+        outs[runner] = out
+    a, b = outs["native"], outs["python"]
+    assert open(a + ".ark", "rb").read() == open(b + ".ark", "rb").read()
+    assert open(a + ".len").read() == open(b + ".len").read()
+    ka = [(l.split()[0], l.split()[1].rsplit(":", 1)[1]) for l in open(a + ".scp")]
+    kb = [(l.split()[0], l.split()[1].rsplit(":", 1)[1]) for l in open(b + ".scp")]
+    assert ka == kb
+
+
+@RUNNERS
+def test_cli_diff_and_noise(tmp_path, monkeypatch, runner):
     meta, sig, ref, z = load_golden("wsj_diff")
     scp = _write_scp(str(tmp_path), sig, meta["utts"])
     out = str(tmp_path / "d")
-    getFeats(_args([scp, out] + _opts(meta) + ["--add_noise=diff"]))
+    _run([scp, out] + _opts(meta) + ["--add_noise=diff"], runner)
     _check(out, meta, ref, meta["utts"])
 
     meta, sig, ref, z = load_golden("chime4_noise")
@@ -104,8 +219,8 @@ def test_cli_diff_and_noise(tmp_path, monkeypatch):
     scp = _write_scp(str(d), sig, meta["utts"])
     monkeypatch.chdir(str(d))
     out = str(d / "nz")
-    getFeats(_args([scp, out] + _opts(meta) + ["--add_noise=babble,20",
-                                                "--noise_seed=%d" % meta["extra"]["noise_seed"]]))
+    _run([scp, out] + _opts(meta) + ["--add_noise=babble,20", "--noise_seed=%d" % meta["extra"]["noise_seed"]],
+         runner)
     _check(out, meta, ref, meta["utts"])
 
 

@@ -197,6 +197,47 @@ def test_wav_parser_matches_scipy(tmp_path):
     assert np.array_equal(y, x)
 
 
+def test_wav_decoder_matches_scipy_formats(tmp_path):
+    """fdlp_wav_decode returns scipy.io.wavfile.read's values for every format scipy reads (the
+    reference featurises them unscaled, computeFDLPSpectrogram.py:139,:156-157): 8-bit unsigned, 16/32-bit
+    int, 24-bit (left-justified int32), float32/64, WAVE_FORMAT_EXTENSIBLE, big-endian RIFX, stereo."""
+    from scipy.io.wavfile import read
+    from speech_recognition_tools_amd.featgen.features import read_wav_bytes
+    rng = np.random.default_rng(3)
+    x = np.clip(rng.standard_normal(777) * 5000, -32768, 32767).astype(np.int16)
+    cases = {"u8": (x // 256 + 128).astype(np.uint8), "i32": x.astype(np.int32) * 65537,
+             "f32": (x / 32768.0).astype(np.float32), "f64": x / 7.0, "i16": x,
+             "stereo": np.stack([x, -x], axis=1)}
+    for name, v in cases.items():
+        p = str(tmp_path / (name + ".wav"))
+        wavfile.write(p, 16000, v)
+        raw = open(p, "rb").read()
+        sr, got = read_wav_bytes(raw)
+        sr2, want = read(p)
+        assert sr == sr2 == 16000 and got.shape == want.shape, name
+        assert (got.dtype == np.int16) == (want.dtype == np.int16), name
+        np.testing.assert_array_equal(got, want.astype(got.dtype), err_msg=name)
+    # 24-bit PCM, plain and WAVE_FORMAT_EXTENSIBLE, little- and big-endian
+    v = x.astype(np.int32) * 256 + 5
+    for ext in (False, True):
+        for big in (False, True):
+            e = ">" if big else "<"
+            raw = b"".join(struct.pack(e + "i", int(s))[1:] if big else struct.pack("<i", int(s))[:3] for s in v)
+            if ext:
+                tail = (b"\x00\x00\x00\x10" if big else b"\x00\x00\x10\x00") + b"\x80\x00\x00\xAA\x00\x38\x9B\x71"
+                fmt = struct.pack(e + "HHIIHHHHII", 0xFFFE, 1, 16000, 48000, 3, 24, 22, 24, 4, 1) + tail
+            else:
+                fmt = struct.pack(e + "HHIIHH", 1, 1, 16000, 48000, 3, 24)
+            body = b"WAVE" + b"fmt " + struct.pack(e + "I", len(fmt)) + fmt + b"data" + struct.pack(e + "I", len(raw)) + raw
+            blob = (b"RIFX" if big else b"RIFF") + struct.pack(e + "I", len(body)) + body
+            p = str(tmp_path / ("i24_%d_%d.wav" % (ext, big)))
+            open(p, "wb").write(blob)
+            sr, got = read_wav_bytes(blob)
+            sr2, want = read(p)
+            assert want.dtype.kind == "i" and want.dtype.itemsize == 4
+            np.testing.assert_array_equal(got, want.astype(np.float64))
+
+
 def test_wav_parser_rejects_garbage():
     from speech_recognition_tools_amd import FdlpError
     from speech_recognition_tools_amd.featgen.features import read_wav_bytes
@@ -221,6 +262,24 @@ def test_ark_writer_roundtrip_and_scp_offsets(tmp_path):
         assert os.path.isabs(path) and os.path.samefile(path, out + ".ark")
         assert data[int(off):int(off) + 2] == b"\0B"
         assert data[int(off) - len(key) - 1:int(off)] == (key + " ").encode()
+    assert not any(f.endswith(".tmp") for f in os.listdir(str(tmp_path)))  # written to .tmp, renamed on close
+
+
+def test_ark_writer_is_atomic(tmp_path):
+    """Until fdlp_ark_close the ark/scp exist only as <name>.tmp (a JOB's outputs appear complete or not
+    at all), and the scp already names the final ark path."""
+    import ctypes
+    from speech_recognition_tools_amd._lib import check, lib
+    h = ctypes.c_void_p()
+    out = str(tmp_path / "j.1")
+    check(lib.fdlp_ark_open((out + ".ark").encode(), (out + ".scp").encode(), ctypes.byref(h)))
+    m = np.ones((2, 3), dtype=np.float32)
+    check(lib.fdlp_ark_write(h, b"u", m.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), 2, 3))
+    assert sorted(os.listdir(str(tmp_path))) == ["j.1.ark.tmp", "j.1.scp.tmp"]
+    check(lib.fdlp_ark_close(h))
+    assert sorted(os.listdir(str(tmp_path))) == ["j.1.ark", "j.1.scp"]
+    line = open(out + ".scp").read().split()
+    assert line[1].rsplit(":", 1)[0] == os.path.realpath(out + ".ark")
 
 
 def test_cli_argparse_surface_matches_reference():
