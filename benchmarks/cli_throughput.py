@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--runners", nargs="+", default=["native", "python"], choices=["native", "python"])
     a = ap.parse_args()
     from bench import speech_like_batch
+    from speech_recognition_tools_amd.featgen import computeFDLPSpectrogram as cli
     from speech_recognition_tools_amd.featgen.computeFDLPSpectrogram import build_parser, getFeats
     T = int(a.seconds * 16000)
     with tempfile.TemporaryDirectory() as d:
@@ -74,7 +75,8 @@ def main():
                               "value": audio_h / el, "unit": "audio-hours/s", "io_workers": w,
                               "host_runner": runner,
                               "utts": a.utts, "utt_seconds": a.seconds, "seconds": el,
-                              "ark_bytes": os.path.getsize(os.path.join(d, "o%d.ark" % w))}))
+                              "ark_bytes": os.path.getsize(os.path.join(d, "o%d.ark" % w)),
+                              "job_stats": cli.LAST_JOB_STATS if runner == "native" else None}))
             sys.stdout.flush()
 
 

@@ -336,6 +336,10 @@ typedef struct fdlp_job_stats {
   int64_t n_frames_out;        /* feature rows written                         */
   int64_t n_samples;           /* samples featurised                           */
   double seconds;              /* wall time of the call                        */
+  double setup_seconds;        /* plan creation, buffers, output files          */
+  double read_wait_seconds;    /* consumer waiting for the reader threads       */
+  double write_seconds;        /* writer thread busy (ark/scp/len)              */
+  double slot_wait_seconds;    /* consumer waiting for a free batch slot        */
 } fdlp_job_stats;
 int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_path, const char* outfile,
                  const fdlp_job_opts* opts, fdlp_job_stats* stats);

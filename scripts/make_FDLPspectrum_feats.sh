@@ -1,8 +1,9 @@
 #!/usr/bin/env bash
 # Drop-in for recipes/timit/local_pyspeech/make_FDLPspectrum_feats.sh of
 # sadhusamik/speech_recognition_tools (same options and outputs), running each JOB's
-# compute-fdlp-feats on an MI355X.  Extra option: --ngpu N (JOBs are assigned round-robin to
-# GPUs 0..N-1 through HIP_VISIBLE_DEVICES; at most N JOBs run at once when no Kaldi $cmd is used).
+# compute-fdlp-feats on an MI355X.  Extra options: --ngpu N (JOB n runs on GPU (n-1) mod N, with or
+# without a Kaldi $cmd launcher: the CLI gets --device_rr=JOB,N and picks the device before any GPU
+# call), --jobs_per_gpu K (without $cmd: at most N*K JOBs run at once; default 1).
 #
 #   make_FDLPspectrum_feats.sh [--opts] <data_dir> <feat_dir>
 # Inputs: <data_dir>/wav.scp or <data_dir>/segments.  Outputs: <data_dir>/feats.scp,
@@ -31,6 +32,7 @@ write_utt2num_frames=false
 lifter_config=
 check_for_segment="data/train"
 ngpu=1
+jobs_per_gpu=1
 compute_cmvn=false   # also write <data_dir>/cmvn.ark (global CMVN stats, fused on the device)
 seed=
 noise_seed=
@@ -86,7 +88,7 @@ run_jobs() {  # run_jobs <list-pattern containing JOB> <scp-type-opt>
   $compute_cmvn && cmvn_opt="--cmvn_stats $feat_dir/cmvn_${name}.JOB.mat"
   if [ -n "$cmd" ]; then
     $cmd JOB=1:$nj "$log_dir/feats_${name}.JOB.log" \
-      python3 "$cli" "$pattern" "$feat_dir/melspec_${name}.JOB" $add_opts $cmvn_opt $stype \
+      python3 "$cli" "$pattern" "$feat_dir/melspec_${name}.JOB" $add_opts $cmvn_opt $stype --device_rr=JOB,$ngpu \
         --fbank_type=$fbank_type --gamma_weight=$gamma_weight --add_reverb=$add_reverb \
         --add_noise=$add_noise --coeff_num=$coeff_num --coeff_range=$coeff_range --order=$order \
         --overlap_fraction=$overlap_fraction --nfilters=$nfilters --fduration=$fduration \
@@ -95,14 +97,13 @@ run_jobs() {  # run_jobs <list-pattern containing JOB> <scp-type-opt>
   fi
   local pids=() n fail=0
   for n in $(seq $nj); do
-    local g=$(( (n - 1) % ngpu ))
-    HIP_VISIBLE_DEVICES=$g python3 "$cli" "${pattern//JOB/$n}" "$feat_dir/melspec_${name}.$n" $add_opts ${cmvn_opt//JOB/$n} $stype \
+    python3 "$cli" "${pattern//JOB/$n}" "$feat_dir/melspec_${name}.$n" $add_opts ${cmvn_opt//JOB/$n} $stype --device_rr=$n,$ngpu \
       --fbank_type=$fbank_type --gamma_weight=$gamma_weight --add_reverb=$add_reverb \
       --add_noise=$add_noise --coeff_num=$coeff_num --coeff_range=$coeff_range --order=$order \
       --overlap_fraction=$overlap_fraction --nfilters=$nfilters --fduration=$fduration \
       --frate=$frate > "$log_dir/feats_${name}.$n.log" 2>&1 &
     pids+=($!)
-    if [ ${#pids[@]} -ge $ngpu ]; then
+    if [ ${#pids[@]} -ge $(( ngpu * jobs_per_gpu )) ]; then
       wait "${pids[0]}" || fail=1
       pids=("${pids[@]:1}")
     fi

@@ -33,6 +33,12 @@ namespace {
 
 using fdlp::fail;
 
+double now_s() {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
 // ---- one scp entry ---------------------------------------------------------------------------
 struct Utt {
   std::string id;
@@ -263,9 +269,9 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   if (o->scp_type != 0 && o->scp_type != 1) return fail(FDLP_E_INVALID, "Invalid type of scp type, it should be either wav or segment");
   if (cfg->mode != FDLP_MODE_SPECTROGRAM) return fail(FDLP_E_INVALID, "fdlp_job_run: spectrogram plans only");
   if (o->noise && o->preprocess == FDLP_PRE_DIFF) return fail(FDLP_E_INVALID, "fdlp_job_run: diff and noise are exclusive");
-  struct timespec t0;
-  clock_gettime(CLOCK_MONOTONIC, &t0);
+  const double t_start = now_s();
   fdlp_job_stats stats{};
+  double write_busy = 0.0;
 
   // scp lines (for line in fid: every line, blank lines included, is an entry of the reference; a
   // blank line raises IndexError there; here blank lines are ignored like the Python drop-in)
@@ -343,9 +349,8 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     }
     fdlp_plan_destroy(plan);
     if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
-    struct timespec t1;
-    clock_gettime(CLOCK_MONOTONIC, &t1);
-    stats.seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    stats.seconds = now_s() - t_start;
+    stats.write_seconds = write_busy;
     if (st) *st = stats;
     if (code != FDLP_OK) fdlp::last_error_slot() = keep;
     return code;
@@ -387,6 +392,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
         err = FDLP_E_HIP;
         msg = "device batch failed";
       }
+      const double tb = now_s();
       for (size_t i = 0; i < d.ids.size() && err == FDLP_OK; ++i) {
         const int64_t r0 = d.rows[i], r1 = d.rows[i + 1];
         if (fdlp_ark_write(ark, d.ids[i].c_str(), sl.h_out + r0 * B, (int32_t)(r1 - r0), B) != FDLP_OK) {
@@ -395,6 +401,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
         }
         if (o->write_len) len_text += d.ids[i] + " " + std::to_string(r1 - r0) + "\n";  // :235-236
       }
+      write_busy += now_s() - tb;
       {
         std::lock_guard<std::mutex> g(js.m);
         sl.busy = false;
@@ -421,8 +428,10 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
 
   // waits until the slot's previous batch is written, then makes it the current one
   auto acquire_slot = [&](int k) -> int {
+    const double ta = now_s();
     std::unique_lock<std::mutex> g(js.m);
     js.cv.wait(g, [&] { return !slots[k].busy || js.err != FDLP_OK; });
+    stats.slot_wait_seconds += now_s() - ta;
     if (js.err != FDLP_OK) return fail(js.err, js.err_msg);
     return FDLP_OK;
   };
@@ -482,8 +491,11 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
 
   std::vector<size_t> hout_cap(slots.size(), 0);  // bytes of each slot's pinned output
 
+  stats.setup_seconds = now_s() - t_start;
   for (size_t i = 0; i < reader.size(); ++i) {
+    const double tw = now_s();
     Utt& u = reader.get(i);
+    stats.read_wait_seconds += now_s() - tw;
     const bool skip = !u.ok;
     if (!skip) sr_seen = u.sr;
     if (o->scp_type == 0) {

@@ -54,6 +54,9 @@ def build_parser():
     parser.add_argument('--seed', type=int, default=None, help='seed of the OLA hop jitter (random.seed)')
     parser.add_argument('--noise_seed', type=int, default=None, help='seed of the noise offsets (np.random.seed)')
     parser.add_argument('--device', type=int, default=None, help='HIP device (default: LOCAL_RANK or 0)')
+    parser.add_argument('--device_rr', type=str, default=None,
+                        help='"JOB,N": run on device (JOB-1) mod N (what make_FDLPspectrum_feats.sh --ngpu N '
+                             'passes, so Kaldi $cmd array jobs spread over the GPUs)')
     parser.add_argument('--batch_frames', type=int, default=8192, help='analysis frames per GPU batch')
     parser.add_argument('--ark_precision', type=int, default=3,
                         help="decimals of the reference's text ark ('%%.3f'); -1 keeps full float32")
@@ -69,6 +72,18 @@ def build_parser():
                              'pinned double-buffered batches, writer thread); python: the same loop in Python '
                              '(always used with --add_reverb)')
     return parser
+
+
+def resolve_device(args):
+    """--device, else --device_rr "JOB,N" -> (JOB-1) mod N, else LOCAL_RANK, else 0."""
+    if args.device is not None:
+        return int(args.device)
+    if getattr(args, 'device_rr', None):
+        job, n = (int(v) for v in args.device_rr.split(','))
+        if job < 1 or n < 1:
+            raise ValueError('--device_rr needs JOB >= 1 and N >= 1')
+        return (job - 1) % n
+    return int(os.environ.get("LOCAL_RANK", "0"))
 
 
 def _read_scp_entry(line, scp_type):
@@ -115,7 +130,7 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
     if scp_type not in ('wav', 'segment'):
         raise ValueError('Invalid type of scp type, it should be either wav or segment')
 
-    device = args.device if args.device is not None else int(os.environ.get("LOCAL_RANK", "0"))
+    device = resolve_device(args)
     if getattr(args, 'host_runner', 'python') == 'native' and rir is None and not return_feats:
         return _run_native(args, cfg, device, noise, snr if noise is not None else 0.0, diff)
     torch.cuda.set_device(device)
@@ -286,7 +301,8 @@ def _run_native(args, cfg, device, noise, snr, diff):
     hold.append(key)
     o.jitter_key, o.jitter_key_len = _lib.ptr(key, ctypes.c_uint32), key.size
     o.srate = 16000
-    o.progress_name = sys.argv[0].encode()
+    # the reference's progress lines, from the C runtime's stdout (only when Python's stdout is the process's)
+    o.progress_name = sys.argv[0].encode() if sys.stdout is sys.__stdout__ else None
     o.cmvn_path = args.cmvn_stats.encode() if args.cmvn_stats else None
     st = _lib.FdlpJobStatsC()
     sys.stdout.flush()
@@ -299,8 +315,13 @@ def _run_native(args, cfg, device, noise, snr, diff):
         if msg == 'Input file has different sampling rate.':
             raise AssertionError(msg)                                       # :144
         _lib.check(rc)
+    global LAST_JOB_STATS
+    LAST_JOB_STATS = {k: getattr(st, k) for k, _ in st._fields_}
     _report_skips(st.n_lines, st.n_skipped)
     return None
+
+
+LAST_JOB_STATS = None  # fdlp_job_stats of the last native run (benchmarks/cli_throughput.py reports it)
 
 
 def main(argv=None):

@@ -1,0 +1,49 @@
+"""scripts/make_FDLPspectrum_feats.sh on the CPU: with a Kaldi-style $cmd launcher (--cmd run.pl-like)
+every JOB gets --device_rr=JOB,<ngpu> so JOB n runs on GPU (n-1) mod ngpu (the reference's recipes call
+the driver with --cmd "$train_cmd", e2e/wsj/run_fdlp_e1.sh:189-209); the CLI resolves it before any GPU
+call.  A fake run.pl records the command lines instead of running them."""
+import os
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+
+def _resolve(argv):
+    from speech_recognition_tools_amd.featgen.computeFDLPSpectrogram import build_parser, resolve_device
+    return resolve_device(build_parser().parse_args(argv))
+
+
+def test_resolve_device_options(monkeypatch):
+    monkeypatch.delenv("LOCAL_RANK", raising=False)
+    assert _resolve(["a.scp", "o"]) == 0
+    assert _resolve(["a.scp", "o", "--device_rr=7,4"]) == 2
+    assert _resolve(["a.scp", "o", "--device_rr=7,4", "--device=1"]) == 1
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    assert _resolve(["a.scp", "o"]) == 3
+    with pytest.raises(ValueError):
+        _resolve(["a.scp", "o", "--device_rr=0,4"])
+
+
+@pytest.mark.parametrize("nj,ngpu", [(5, 2), (4, 8)])
+def test_driver_cmd_branch_spreads_jobs_over_gpus(tmp_path, nj, ngpu):
+    data = tmp_path / "data" / "dev"
+    data.mkdir(parents=True)
+    (data / "wav.scp").write_text("".join("u%d /x/u%d.wav\n" % (i, i) for i in range(nj * 2)))
+    log = tmp_path / "cmd.log"
+    env = dict(os.environ, FAKE_CMD_LOG=str(log))
+    cmd = ["bash", os.path.join(ROOT, "scripts", "make_FDLPspectrum_feats.sh"), "--nj", str(nj), "--ngpu", str(ngpu),
+           "--cmd", os.path.join(ROOT, "tests", "fakes", "fake_run_pl.sh"), "--write_utt2num_frames", "true",
+           str(data), str(tmp_path / "fbank")]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = log.read_text().splitlines()
+    assert len(lines) == nj
+    devices = []
+    for n, line in enumerate(lines, 1):
+        argv = line.split()[2:]  # drop "python3 <cli>"
+        assert argv[1].endswith("melspec_dev.%d" % n)
+        assert "--device_rr=%d,%d" % (n, ngpu) in argv
+        devices.append(_resolve(argv))
+    assert devices == [(n - 1) % ngpu for n in range(1, nj + 1)]
