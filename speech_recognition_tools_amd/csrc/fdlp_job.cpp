@@ -21,6 +21,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -46,8 +47,71 @@ struct Utt {
   bool is_int16 = false;
   int32_t sr = 0, ch = 0;
   int64_t T = 0;
-  std::vector<int16_t> s16;   // is_int16
-  std::vector<double> f64;    // otherwise (scipy's dtype, converted exactly as numpy does)
+  std::shared_ptr<std::vector<uint8_t>> raw;   // the file bytes; is_int16: the samples point into them
+  const int16_t* s16 = nullptr;
+  std::shared_ptr<std::vector<double>> f64;    // otherwise (scipy's dtype, converted exactly as numpy does)
+};
+
+// memcpy jobs (utterance samples -> the pinned batch buffer) on a few threads; a job keeps its source alive
+class CopyPool {
+ public:
+  explicit CopyPool(int n) {
+    for (int t = 0; t < n; ++t) th_.emplace_back([this] { run(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void submit(int tag, void* dst, const void* src, size_t n, std::shared_ptr<void> keep) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back(Job{tag, dst, src, n, std::move(keep)});
+      ++pending_[tag];
+    }
+    cv_.notify_one();
+  }
+  void wait(int tag) {
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [&] { return pending_[tag] == 0; });
+  }
+
+ private:
+  struct Job {
+    int tag;
+    void* dst;
+    const void* src;
+    size_t n;
+    std::shared_ptr<void> keep;
+  };
+  void run() {
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        j = std::move(q_.front());
+        q_.pop_front();
+      }
+      memcpy(j.dst, j.src, j.n);
+      j.keep.reset();
+      {
+        std::lock_guard<std::mutex> g(m_);
+        --pending_[j.tag];
+      }
+      done_.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  std::deque<Job> q_;
+  int pending_[8] = {0};
+  bool stop_ = false;
+  std::vector<std::thread> th_;
 };
 
 bool read_file(const std::string& path, int64_t offset, std::vector<uint8_t>& out) {
@@ -121,25 +185,25 @@ void read_entry(const std::string& line, Utt& u) {
   u.id = tok.empty() ? std::string() : tok[0];
   std::string rx;
   for (size_t k = 1; k < tok.size(); ++k) rx += (k > 1 ? " " : "") + tok[k];
-  std::vector<uint8_t> bytes;
-  if (tok.size() < 2 || !read_rx_bytes(rx, bytes)) return;
+  auto bytes = std::make_shared<std::vector<uint8_t>>();
+  if (tok.size() < 2 || !read_rx_bytes(rx, *bytes)) return;
   int32_t sr = 0, ch = 0, i16 = 0;
   int64_t n = 0;
-  if (fdlp_wav_decode(bytes.data(), (int64_t)bytes.size(), &sr, &ch, &i16, &n, nullptr) != FDLP_OK) return;
+  if (fdlp_wav_decode(bytes->data(), (int64_t)bytes->size(), &sr, &ch, &i16, &n, nullptr) != FDLP_OK) return;
   u.sr = sr;
   u.ch = ch;
   u.T = n;
   u.is_int16 = i16 != 0;
-  if (u.is_int16) {
+  if (u.is_int16) {  // the samples stay in the file bytes (no copy until the batch buffer)
     int32_t s2, c2;
     int64_t n2;
     const int16_t* smp = nullptr;
-    if (fdlp_wav_parse(bytes.data(), (int64_t)bytes.size(), &s2, &c2, &smp, &n2) != FDLP_OK) return;
-    u.s16.resize((size_t)n * ch);
-    memcpy(u.s16.data(), smp, sizeof(int16_t) * u.s16.size());
+    if (fdlp_wav_parse(bytes->data(), (int64_t)bytes->size(), &s2, &c2, &smp, &n2) != FDLP_OK) return;
+    u.s16 = smp;
+    u.raw = std::move(bytes);
   } else {
-    u.f64.resize((size_t)n * ch);
-    if (fdlp_wav_decode(bytes.data(), (int64_t)bytes.size(), nullptr, nullptr, nullptr, nullptr, u.f64.data()) !=
+    u.f64 = std::make_shared<std::vector<double>>((size_t)n * ch);
+    if (fdlp_wav_decode(bytes->data(), (int64_t)bytes->size(), nullptr, nullptr, nullptr, nullptr, u.f64->data()) !=
         FDLP_OK)
       return;
   }
@@ -224,7 +288,9 @@ struct Slot {
   float* h_out = nullptr;      // pinned
   float* d_out = nullptr;
   size_t out_cap = 0;          // floats
-  hipEvent_t done = nullptr;
+  hipEvent_t done = nullptr;     // the batch's features are in h_out
+  hipEvent_t ev_in = nullptr;    // its PCM is on the device
+  hipEvent_t ev_comp = nullptr;  // its features are computed
   bool busy = false;           // in flight or not yet written
 };
 
@@ -294,6 +360,8 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   }
   stats.n_lines = (int64_t)lines.size();
 
+  Reader reader(lines, std::max(1, o->io_threads), 64);  // reading starts while the plan is built
+
   fdlp_config c = *cfg;
   c.max_frames = std::max(1, o->batch_frames);
   fdlp_plan* plan = nullptr;
@@ -304,13 +372,14 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
 
   int prev_dev = -1;
   (void)hipGetDevice(&prev_dev);
-  hipStream_t s = nullptr;
+  hipStream_t s = nullptr, s_in = nullptr, s_out = nullptr;  // compute, copy-in, copy-out
   fdlp_pyrandom* jrng = nullptr;
   fdlp_nprandom* nrng = nullptr;
   fdlp_ark_writer* ark = nullptr;
   int16_t* d_noise = nullptr;
   double* d_cmvn = nullptr;
   std::vector<Slot> slots(3);
+  CopyPool copies(4);  // before cleanup(): drained there before the pinned buffers are freed
   JobState js;
   js.slots = &slots;
   std::string len_text;
@@ -328,16 +397,23 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
       writer.join();
     }
     if (s) (void)hipStreamSynchronize(s);
+    if (s_in) (void)hipStreamSynchronize(s_in);
+    if (s_out) (void)hipStreamSynchronize(s_out);
+    for (int k = 0; k < (int)slots.size(); ++k) copies.wait(k);
     for (auto& sl : slots) {
       if (sl.h_pcm) (void)hipHostFree(sl.h_pcm);
       if (sl.h_out) (void)hipHostFree(sl.h_out);
       if (sl.d_pcm) (void)hipFree(sl.d_pcm);
       if (sl.d_out) (void)hipFree(sl.d_out);
       if (sl.done) (void)hipEventDestroy(sl.done);
+      if (sl.ev_in) (void)hipEventDestroy(sl.ev_in);
+      if (sl.ev_comp) (void)hipEventDestroy(sl.ev_comp);
     }
     if (d_noise) (void)hipFree(d_noise);
     if (d_cmvn) (void)hipFree(d_cmvn);
     if (s) (void)hipStreamDestroy(s);
+    if (s_in) (void)hipStreamDestroy(s_in);
+    if (s_out) (void)hipStreamDestroy(s_out);
     if (jrng) fdlp_pyrandom_destroy(jrng);
     if (nrng) fdlp_nprandom_destroy(nrng);
     if (ark) {
@@ -360,7 +436,13 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
 
   JOB_HIP(hipSetDevice(device));
   JOB_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  for (auto& sl : slots) JOB_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  JOB_HIP(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking));
+  JOB_HIP(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking));
+  for (auto& sl : slots) {
+    JOB_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    JOB_HIP(hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming));
+    JOB_HIP(hipEventCreateWithFlags(&sl.ev_comp, hipEventDisableTiming));
+  }
   JOB_TRY(fdlp_pyrandom_create(o->jitter_key, o->jitter_key_len, &jrng));
   if (o->noise) {
     JOB_TRY(fdlp_nprandom_create(o->noise_seed, &nrng));
@@ -414,7 +496,6 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     }
   });
 
-  Reader reader(lines, std::max(1, o->io_threads), 64);
   const size_t pcm_elem_i16 = sizeof(int16_t), pcm_elem_f64 = sizeof(double);
   struct Pending {
     std::vector<std::string> ids;
@@ -441,11 +522,14 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     if (pend.ids.empty()) return FDLP_OK;
     Slot& sl = slots[slot_i];
     const size_t elem = pend.kind == FDLP_PCM_I16 ? pcm_elem_i16 : pcm_elem_f64;
+    copies.wait(slot_i);  // every utterance of the batch is in the pinned buffer
     int r = grow_device(&sl.d_pcm, &sl.d_pcm_cap, (size_t)pend.samples * elem, s);
     if (r != FDLP_OK) return r;
     r = grow_device((void**)&sl.d_out, &sl.out_cap, sizeof(float) * (size_t)pend.out_rows * B, s);
     if (r != FDLP_OK) return r;
-    if (hipMemcpyAsync(sl.d_pcm, sl.h_pcm, (size_t)pend.samples * elem, hipMemcpyHostToDevice, s) != hipSuccess)
+    // copy-in on its own stream so it overlaps the previous batch's kernels
+    if (hipMemcpyAsync(sl.d_pcm, sl.h_pcm, (size_t)pend.samples * elem, hipMemcpyHostToDevice, s_in) != hipSuccess ||
+        hipEventRecord(sl.ev_in, s_in) != hipSuccess || hipStreamWaitEvent(s, sl.ev_in, 0) != hipSuccess)
       return fail(FDLP_E_HIP, "H2D copy failed");
     fdlp_batch b{};
     b.n_utt = (int32_t)pend.ids.size();
@@ -468,9 +552,11 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
       r = fdlp_cmvn_accumulate(sl.d_out, pend.out_rows, B, d_cmvn, s);
       if (r != FDLP_OK) return r;
     }
-    if (hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * (size_t)pend.out_rows * B, hipMemcpyDeviceToHost, s) !=
+    // copy-out on its own stream so it overlaps the next batch's kernels
+    if (hipEventRecord(sl.ev_comp, s) != hipSuccess || hipStreamWaitEvent(s_out, sl.ev_comp, 0) != hipSuccess ||
+        hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * (size_t)pend.out_rows * B, hipMemcpyDeviceToHost, s_out) !=
             hipSuccess ||
-        hipEventRecord(sl.done, s) != hipSuccess)
+        hipEventRecord(sl.done, s_out) != hipSuccess)
       return fail(FDLP_E_HIP, "D2H copy failed");
     Done d;
     d.slot = slot_i;
@@ -490,6 +576,20 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   };
 
   std::vector<size_t> hout_cap(slots.size(), 0);  // bytes of each slot's pinned output
+  {  // pinned and device buffers of a full int16 batch, allocated up front (growth stays possible)
+    int32_t N_, hop = 0, nl_, kk_, oh_;
+    fdlp_plan_info(plan, &N_, &hop, &nl_, &kk_, &oh_);
+    const size_t smp = (size_t)c.max_frames * (size_t)(hop + 1);
+    const size_t rows = (size_t)c.max_frames * (size_t)((int64_t)hop * c.frate / std::max(1, c.srate) + 2);
+    for (size_t k = 0; k < slots.size(); ++k) {
+      Slot& sl = slots[k];
+      JOB_TRY(grow_pinned(&sl.h_pcm, &sl.pcm_cap, smp * sizeof(int16_t)));
+      JOB_HIP(hipHostMalloc((void**)&sl.h_out, rows * B * sizeof(float), hipHostMallocDefault));
+      hout_cap[k] = rows * B * sizeof(float);
+      JOB_TRY(grow_device(&sl.d_pcm, &sl.d_pcm_cap, smp * sizeof(int16_t), s));
+      JOB_TRY(grow_device((void**)&sl.d_out, &sl.out_cap, rows * B * sizeof(float), s));
+    }
+  }
 
   stats.setup_seconds = now_s() - t_start;
   for (size_t i = 0; i < reader.size(); ++i) {
@@ -520,7 +620,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     if (o->noise) {  // add_noise_to_wav (features.py:24-31), np.random.rand() per utterance (:166)
       double uu = 0.0;
       JOB_TRY(fdlp_nprandom_rand(nrng, 1, &uu));
-      JOB_TRY(fdlp_noise_params(u.s16.data(), T, o->noise, o->noise_len, o->snr, uu, &noff, &alpha));
+      JOB_TRY(fdlp_noise_params(u.s16, T, o->noise, o->noise_len, o->snr, uu, &noff, &alpha));
     }
     if (o->progress_name) printf("%s: Computing Features for file: %s\n", o->progress_name, u.id.c_str());  // :185
     // a batch is one PCM kind and at most max_frames frames
@@ -543,13 +643,16 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     const size_t elem = kind == FDLP_PCM_I16 ? pcm_elem_i16 : pcm_elem_f64;
     const size_t need = (size_t)(pend.samples + T) * elem;
     if (need > sl.pcm_cap) {
+      copies.wait(slot_i);  // the pending copies target the old buffer
       std::vector<uint8_t> keep((size_t)pend.samples * elem);
       if (pend.samples) memcpy(keep.data(), sl.h_pcm, keep.size());
       JOB_TRY(grow_pinned(&sl.h_pcm, &sl.pcm_cap, std::max(need, (size_t)c.max_frames * 18000 * elem)));
       if (!keep.empty()) memcpy(sl.h_pcm, keep.data(), keep.size());
     }
-    if (kind == FDLP_PCM_I16) memcpy((int16_t*)sl.h_pcm + pend.samples, u.s16.data(), sizeof(int16_t) * T);
-    else memcpy((double*)sl.h_pcm + pend.samples, u.f64.data(), sizeof(double) * T);
+    if (kind == FDLP_PCM_I16)
+      copies.submit(slot_i, (int16_t*)sl.h_pcm + pend.samples, u.s16, sizeof(int16_t) * T, u.raw);
+    else
+      copies.submit(slot_i, (double*)sl.h_pcm + pend.samples, u.f64->data(), sizeof(double) * T, u.f64);
     // pinned host output for this batch's rows
     const size_t rows_need = (size_t)(pend.out_rows + L);
     if (rows_need * B * sizeof(float) > hout_cap[slot_i]) {

@@ -57,7 +57,7 @@ def build_parser():
     parser.add_argument('--device_rr', type=str, default=None,
                         help='"JOB,N": run on device (JOB-1) mod N (what make_FDLPspectrum_feats.sh --ngpu N '
                              'passes, so Kaldi $cmd array jobs spread over the GPUs)')
-    parser.add_argument('--batch_frames', type=int, default=8192, help='analysis frames per GPU batch')
+    parser.add_argument('--batch_frames', type=int, default=2048, help='analysis frames per GPU batch')
     parser.add_argument('--ark_precision', type=int, default=3,
                         help="decimals of the reference's text ark ('%%.3f'); -1 keeps full float32")
     parser.add_argument('--support_eps', type=float, default=None,
