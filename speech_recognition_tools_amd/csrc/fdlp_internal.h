@@ -87,6 +87,7 @@ struct DevConsts {
   int lpc_lds_durbin = 0;  // FDLP_LPC_LDS at plan creation: the LDS Durbin instead of the lattice
   int lpc_cep_lds = 0;     // FDLP_CEP_LDS at plan creation: the LDS cepstrum form for every M
   int lpc_slotmajor = 0;   // FDLP_LPC_SLOTMAJOR at plan creation: the slot-major lattice Durbin
+  int dct_generic = 0;     // FDLP_DCT_GENERIC at plan creation: runtime-radix DCT passes for every N
 };
 
 }  // namespace fdlp

@@ -306,6 +306,213 @@ __global__ __launch_bounds__(256) void dft2_dct_kernel(DevConsts c, DftPlan d2, 
 }
 
 // -----------------------------------------------------------------------------------------
+// 1s/2s. The same two DCT passes specialised at compile time for the recipes' frame length
+// (N = 24000: packed length-12000 complex FFT = 100 x 120; radices 4.5.5 and 8.3.5): constant
+// butterflies (roots of unity as literals), constant Stockham strides, COLS interleaved columns
+// (rows) per workgroup, and a branch-free sample gather for frames that need no reflect padding.
+// Same arithmetic order per butterfly as the generic passes (Stockham DIT, twiddle then DFT).
+// -----------------------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ void bfly_c(double2 (&v)[R]) {
+  if constexpr (R == 2) {
+    const double2 a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = make_double2(a.x - b.x, a.y - b.y);
+  } else if constexpr (R == 4) {
+    const double2 a0 = cadd(v[0], v[2]), a1 = make_double2(v[0].x - v[2].x, v[0].y - v[2].y);
+    const double2 b0 = cadd(v[1], v[3]), b1 = make_double2(v[1].x - v[3].x, v[1].y - v[3].y);
+    const double2 b1m = make_double2(b1.y, -b1.x);  // -i b1
+    v[0] = cadd(a0, b0);
+    v[2] = make_double2(a0.x - b0.x, a0.y - b0.y);
+    v[1] = cadd(a1, b1m);
+    v[3] = make_double2(a1.x - b1m.x, a1.y - b1m.y);
+  } else if constexpr (R == 3) {
+    constexpr double c1 = -0.5, s1 = -0.86602540378443864676;  // e^{-2 pi i / 3}
+    const double2 t = cadd(v[1], v[2]);
+    const double2 d = make_double2(v[1].x - v[2].x, v[1].y - v[2].y);
+    const double2 m = make_double2(v[0].x + c1 * t.x, v[0].y + c1 * t.y);
+    const double2 u = make_double2(-s1 * d.y, s1 * d.x);  // i s1 d
+    v[0] = cadd(v[0], t);
+    v[1] = cadd(m, u);
+    v[2] = make_double2(m.x - u.x, m.y - u.y);
+  } else if constexpr (R == 5) {
+    constexpr double c1 = 0.30901699437494742410, s1 = -0.95105651629515357212;  // e^{-2 pi i / 5}
+    constexpr double c2 = -0.80901699437494742410, s2 = -0.58778525229247312917; // e^{-4 pi i / 5}
+    const double2 t1 = cadd(v[1], v[4]), d1 = make_double2(v[1].x - v[4].x, v[1].y - v[4].y);
+    const double2 t2 = cadd(v[2], v[3]), d2 = make_double2(v[2].x - v[3].x, v[2].y - v[3].y);
+    const double2 m1 = make_double2(v[0].x + c1 * t1.x + c2 * t2.x, v[0].y + c1 * t1.y + c2 * t2.y);
+    const double2 m2 = make_double2(v[0].x + c2 * t1.x + c1 * t2.x, v[0].y + c2 * t1.y + c1 * t2.y);
+    // i (s1 d1 + s2 d2) and i (s2 d1 - s1 d2)
+    const double2 u1 = make_double2(-(s1 * d1.y + s2 * d2.y), s1 * d1.x + s2 * d2.x);
+    const double2 u2 = make_double2(-(s2 * d1.y - s1 * d2.y), s2 * d1.x - s1 * d2.x);
+    v[0] = cadd(cadd(v[0], t1), t2);
+    v[1] = cadd(m1, u1);
+    v[4] = make_double2(m1.x - u1.x, m1.y - u1.y);
+    v[2] = cadd(m2, u2);
+    v[3] = make_double2(m2.x - u2.x, m2.y - u2.y);
+  }
+}
+
+// One Stockham stage (radix R, Ns = product of the radices before it) of COLS interleaved length-N
+// columns in LDS; om = the N roots omega_N^q.
+template <int N, int COLS, int NT, int Ns, int R>
+__device__ __forceinline__ void st_stage_c(const double2* __restrict__ in, double2* __restrict__ out,
+                                           const double2* __restrict__ om) {
+  constexpr int NB = N / R, TOT = NB * COLS, ITER = (TOT + NT - 1) / NT, TW0 = N / (Ns * R);
+#pragma unroll
+  for (int it = 0; it < ITER; ++it) {
+    const int b = (int)threadIdx.x + it * NT;
+    if (TOT % NT != 0 && b >= TOT) break;
+    const int col = b % COLS, j = b / COLS;
+    const int k = j % Ns, jq = j / Ns;
+    double2 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const double2 x = in[(j + r * NB) * COLS + col];
+      v[r] = (r == 0 || Ns == 1) ? x : cmul(x, om[TW0 * k * r]);
+    }
+    bfly_c<R>(v);
+    const int idxD = jq * Ns * R + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) out[(idxD + r * Ns) * COLS + col] = v[r];
+  }
+}
+
+// full length-N DFT of COLS columns, radices R0 R1 ...; returns the buffer holding the result
+template <int N, int COLS, int NT, int Ns, int R0, int... Rs>
+__device__ __forceinline__ double2* lds_dft_c(double2* a, double2* b, const double2* om) {
+  st_stage_c<N, COLS, NT, Ns, R0>(a, b, om);
+  __syncthreads();
+  if constexpr (sizeof...(Rs) > 0) return lds_dft_c<N, COLS, NT, Ns * R0, Rs...>(b, a, om);
+  else return b;
+}
+
+template <int N1>
+struct DctRadices1;
+template <>
+struct DctRadices1<100> {
+  template <int COLS, int NT>
+  __device__ static double2* run(double2* a, double2* b, const double2* om) {
+    return lds_dft_c<100, COLS, NT, 1, 4, 5, 5>(a, b, om);
+  }
+};
+template <int N2>
+struct DctRadices2;
+template <>
+struct DctRadices2<120> {
+  template <int COLS, int NT>
+  __device__ static double2* run(double2* a, double2* b, const double2* om) {
+    return lds_dft_c<120, COLS, NT, 1, 4, 2, 3, 5>(a, b, om);
+  }
+};
+
+template <int N1, int N2, int COLS>
+__global__ __launch_bounds__(256) void frames_dft1_c_kernel(DevConsts c, const void* __restrict__ pcm, int pcm_kind,
+                                                            const int16_t* __restrict__ noise,
+                                                            const FrameDesc* __restrict__ frames,
+                                                            const double2* __restrict__ om1,
+                                                            double2* __restrict__ z) {
+  constexpr int NT = 256;
+  __shared__ double2 bufA[N1 * COLS], bufB[N1 * COLS], oms[N1];
+  const int f = blockIdx.y;
+  const int n2_0 = blockIdx.x * COLS;
+  for (int q = threadIdx.x; q < N1; q += NT) oms[q] = om1[q];
+  const FrameDesc fd = frames[f];
+  const int N = c.N;
+  const int64_t t0 = (int64_t)fd.k * c.hop - c.ext;
+  // no reflect padding, plain int16, no mixing: sample m of the frame is pcm[pcm_off + t0 + m]
+  const bool fast = pcm_kind == 0 && fd.noise_off < 0 && t0 >= 0 && t0 + N <= fd.T;
+  const int16_t* xs = (const int16_t*)pcm + fd.pcm_off + t0;
+  constexpr int TOT = N1 * COLS;
+#pragma unroll
+  for (int it = 0; it < (TOT + NT - 1) / NT; ++it) {
+    const int e = (int)threadIdx.x + it * NT;
+    if (TOT % NT != 0 && e >= TOT) break;
+    const int col = e % COLS, n1 = e / COLS;
+    const int q = N2 * n1 + n2_0 + col;  // packed z[q] = v[2q] + i v[2q+1] (Makhoul order v)
+    const int m0 = 4 * q < N ? 4 * q : 2 * N - 1 - 4 * q;
+    const int m1 = 4 * q + 2 < N ? 4 * q + 2 : 2 * N - 3 - 4 * q;
+    double2 val;
+    if (fast) {
+      val.x = __dmul_rn((double)xs[m0], c.hamming[m0]);
+      val.y = __dmul_rn((double)xs[m1], c.hamming[m1]);
+    } else {
+      val.x = makhoul_sample(c, fd, 2 * q, f, pcm, pcm_kind, noise, nullptr);
+      val.y = makhoul_sample(c, fd, 2 * q + 1, f, pcm, pcm_kind, noise, nullptr);
+    }
+    bufA[n1 * COLS + col] = val;
+  }
+  __syncthreads();
+  const double2* res = DctRadices1<N1>::template run<COLS, NT>(bufA, bufB, oms);
+  const double2* tw1 = (const double2*)c.tw1;
+#pragma unroll
+  for (int it = 0; it < (TOT + NT - 1) / NT; ++it) {
+    const int e = (int)threadIdx.x + it * NT;
+    if (TOT % NT != 0 && e >= TOT) break;
+    const int col = e % COLS, k1 = e / COLS;
+    const int n2 = n2_0 + col;
+    z[((int64_t)f * N1 + k1) * N2 + n2] = cmul(res[k1 * COLS + col], tw1[k1 * N2 + n2]);
+  }
+}
+
+// rows k1 of pair pp (pp, N1 - pp): slots r (< COLS/2) and r + COLS/2
+template <int N1, int N2, int COLS>
+__global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const double2* __restrict__ z,
+                                                         const double2* __restrict__ om2, double inv_scale_div,
+                                                         double* __restrict__ dct) {
+  constexpr int NT = 256, HALF = COLS / 2;
+  __shared__ double2 bufA[N2 * COLS], bufB[N2 * COLS], oms[N2];
+  const int f = blockIdx.y;
+  const int N = c.N;
+  auto slot_row = [&](int r) -> int {
+    const int pp = blockIdx.x * HALF + (r % HALF);
+    if (2 * pp > N1) return -1;
+    if (r < HALF) return pp;
+    const int m = N1 - pp;
+    return (pp == 0 || m == pp) ? -1 : m;
+  };
+  for (int q = threadIdx.x; q < N2; q += NT) oms[q] = om2[q];
+  constexpr int TOT = N2 * COLS;
+#pragma unroll
+  for (int it = 0; it < (TOT + NT - 1) / NT; ++it) {
+    const int e = (int)threadIdx.x + it * NT;
+    if (TOT % NT != 0 && e >= TOT) break;
+    const int row = e / N2, n2 = e % N2;  // coalesced over n2
+    const int k1 = slot_row(row);
+    double2 v = make_double2(0.0, 0.0);
+    if (k1 >= 0) v = z[((int64_t)f * N1 + k1) * N2 + n2];
+    bufA[n2 * COLS + row] = v;
+  }
+  __syncthreads();
+  const double2* res = DctRadices2<N2>::template run<COLS, NT>(bufA, bufB, oms);
+  const double2* post = (const double2*)c.post;
+  const double2* rtw = (const double2*)c.rtw;
+  constexpr int M = N1 * N2;
+#pragma unroll
+  for (int it = 0; it < (TOT + NT - 1) / NT; ++it) {
+    const int e = (int)threadIdx.x + it * NT;
+    if (TOT % NT != 0 && e >= TOT) break;
+    const int row = e % COLS, k2 = e / COLS;
+    const int k1 = slot_row(row);
+    if (k1 < 0) continue;
+    const int k = k1 + N1 * k2;
+    const double2 V = res[k2 * COLS + row];
+    const int k1m = k1 == 0 ? 0 : N1 - k1;
+    const int k2m = k1 == 0 ? (k2 == 0 ? 0 : N2 - k2) : N2 - 1 - k2;
+    const int rm = k1m == k1 ? row : (row < HALF ? row + HALF : row - HALF);
+    const double2 W = res[k2m * COLS + rm];
+    const double2 E = make_double2(0.5 * (V.x + W.x), 0.5 * (V.y - W.y));
+    const double2 O = make_double2(0.5 * (V.y + W.y), -0.5 * (V.x - W.x));
+    const double2 t = cmul(rtw[k], O);
+    const double2 V1 = make_double2(E.x + t.x, E.y + t.y);
+    const double2 V2 = make_double2(E.x - t.x, E.y - t.y);
+    const double2 w1 = post[k], w2 = post[k + M];
+    dct[(int64_t)f * N + k] = 2.0 * (w1.x * V1.x - w1.y * V1.y) / inv_scale_div;
+    dct[(int64_t)f * N + k + M] = 2.0 * (w2.x * V2.x - w2.y * V2.y) / inv_scale_div;
+  }
+}
+
+// -----------------------------------------------------------------------------------------
 // wave-level helpers
 // -----------------------------------------------------------------------------------------
 __device__ __forceinline__ double wave_sum(double v) {
@@ -2213,6 +2420,11 @@ hipError_t launch_frames_dft1(const DevConsts& c, const DftPlan& d1, int N2, con
   if (nframes <= 0) return hipSuccess;
   dim3 grid((N2 + kDftCols - 1) / kDftCols, nframes);
   size_t lds = sizeof(double2) * (2 * d1.n * kDftCols + d1.n);
+  if (c.real_fft && !c.dct_generic && d1.n == 100 && N2 == 120 && !dense_rows) {  // recipes: N = 24000
+    hipLaunchKernelGGL((frames_dft1_c_kernel<100, 120, kDftCols>), grid, dim3(256), 0, s, c, pcm, pcm_kind, noise,
+                       frames, om1, z);
+    return hipGetLastError();
+  }
   if (c.real_fft) {
     if (lds > 65536) (void)hipFuncSetAttribute((const void*)frames_dft1_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(frames_dft1_kernel<true>, grid, dim3(256), lds, s, c, d1, N2, pcm, pcm_kind, noise,
@@ -2230,6 +2442,11 @@ hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const 
   if (nframes <= 0) return hipSuccess;
   size_t lds = sizeof(double2) * (2 * d2.n * kDftCols + d2.n);
   const double div = sqrt((double)(2 * c.N));
+  if (c.real_fft && !c.dct_generic && N1 == 100 && d2.n == 120) {  // recipes: N = 24000
+    dim3 grid((N1 / 2 + 1 + kDftCols / 2 - 1) / (kDftCols / 2), nframes);
+    hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols>), grid, dim3(256), 0, s, c, z, om2, div, dct);
+    return hipGetLastError();
+  }
   if (c.real_fft) {
     dim3 grid((N1 / 2 + 1 + kDftCols / 2 - 1) / (kDftCols / 2), nframes);  // row pairs (k1, N1-k1)
     if (lds > 65536) (void)hipFuncSetAttribute((const void*)dft2_dct_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -685,6 +685,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
     }
   }
 
+  d.dct_generic = getenv("FDLP_DCT_GENERIC") != nullptr;
   // launch geometry of the persistent LPC kernel for this device (occupancy, large-LDS attribute)
   if (fdlp::prepare_lpc_env(d) != hipSuccess) PLAN_FAIL(FDLP_E_HIP, "LPC kernel launch setup failed");
 
