@@ -456,12 +456,13 @@ __global__ __launch_bounds__(256) void frames_dft1_c_kernel(DevConsts c, const v
 }
 
 // rows k1 of pair pp (pp, N1 - pp): slots r (< COLS/2) and r + COLS/2
-template <int N1, int N2, int COLS>
+template <int N1, int N2, int COLS, bool TWF = true>
 __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const double2* __restrict__ z,
                                                          const double2* __restrict__ om2, double inv_scale_div,
                                                          double* __restrict__ dct) {
   constexpr int NT = 256, HALF = COLS / 2;
   __shared__ double2 bufA[N2 * COLS], bufB[N2 * COLS], oms[N2];
+  __shared__ double2 pw1[N1], pw2[N2], rw1[N1], rw2[N2];  // factored twiddles (TWF)
   const int f = blockIdx.y;
   const int N = c.N;
   auto slot_row = [&](int r) -> int {
@@ -472,12 +473,18 @@ __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const doub
     return (pp == 0 || m == pp) ? -1 : m;
   };
   for (int q = threadIdx.x; q < N2; q += NT) oms[q] = om2[q];
+  if (TWF) {  // post[k] = post[k1] post[N1 k2], rtw[k] = rtw[k1] rtw[N1 k2]  (k = k1 + N1 k2)
+    const double2* post = (const double2*)c.post;
+    const double2* rtw = (const double2*)c.rtw;
+    for (int q = threadIdx.x; q < N1; q += NT) { pw1[q] = post[q]; rw1[q] = rtw[q]; }
+    for (int q = threadIdx.x; q < N2; q += NT) { pw2[q] = post[N1 * q]; rw2[q] = rtw[N1 * q]; }
+  }
   constexpr int TOT = N2 * COLS;
 #pragma unroll
   for (int it = 0; it < (TOT + NT - 1) / NT; ++it) {
     const int e = (int)threadIdx.x + it * NT;
     if (TOT % NT != 0 && e >= TOT) break;
-    const int row = e / N2, n2 = e % N2;  // coalesced over n2
+    const int row = e / N2, n2 = e % N2;  // coalesced over n2 (the row-fastest order measured slower)
     const int k1 = slot_row(row);
     double2 v = make_double2(0.0, 0.0);
     if (k1 >= 0) v = z[((int64_t)f * N1 + k1) * N2 + n2];
@@ -503,10 +510,21 @@ __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const doub
     const double2 W = res[k2m * COLS + rm];
     const double2 E = make_double2(0.5 * (V.x + W.x), 0.5 * (V.y - W.y));
     const double2 O = make_double2(0.5 * (V.y + W.y), -0.5 * (V.x - W.x));
-    const double2 t = cmul(rtw[k], O);
+    double2 rt, w1, w2;
+    if (TWF) {
+      rt = cmul(rw1[k1], rw2[k2]);
+      w1 = cmul(pw1[k1], pw2[k2]);
+      // post[k + M] = post[k] e^{-i pi M / (2N)} = post[k] e^{-i pi / 4}  (M = N / 2)
+      constexpr double h = 0.70710678118654752440;
+      w2 = make_double2(h * (w1.x + w1.y), h * (w1.y - w1.x));
+    } else {
+      rt = rtw[k];
+      w1 = post[k];
+      w2 = post[k + M];
+    }
+    const double2 t = cmul(rt, O);
     const double2 V1 = make_double2(E.x + t.x, E.y + t.y);
     const double2 V2 = make_double2(E.x - t.x, E.y - t.y);
-    const double2 w1 = post[k], w2 = post[k + M];
     dct[(int64_t)f * N + k] = 2.0 * (w1.x * V1.x - w1.y * V1.y) / inv_scale_div;
     dct[(int64_t)f * N + k + M] = 2.0 * (w2.x * V2.x - w2.y * V2.y) / inv_scale_div;
   }
@@ -2444,7 +2462,11 @@ hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const 
   const double div = sqrt((double)(2 * c.N));
   if (c.real_fft && !c.dct_generic && N1 == 100 && d2.n == 120) {  // recipes: N = 24000
     dim3 grid((N1 / 2 + 1 + kDftCols / 2 - 1) / (kDftCols / 2), nframes);
-    hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols>), grid, dim3(256), 0, s, c, z, om2, div, dct);
+    static const bool table_tw = getenv("FDLP_DCT_TABLE_TW") != nullptr;  // A/B knob: full post/rtw tables
+    if (table_tw)
+      hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, false>), grid, dim3(256), 0, s, c, z, om2, div, dct);
+    else
+      hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, true>), grid, dim3(256), 0, s, c, z, om2, div, dct);
     return hipGetLastError();
   }
   if (c.real_fft) {
