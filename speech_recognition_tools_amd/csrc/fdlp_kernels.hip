@@ -413,10 +413,14 @@ __global__ __launch_bounds__(256) void frames_dft1_c_kernel(DevConsts c, const v
                                                             const double2* __restrict__ om1,
                                                             double2* __restrict__ z) {
   constexpr int NT = 256;
-  __shared__ double2 bufA[N1 * COLS], bufB[N1 * COLS], oms[N1];
+  __shared__ double2 bufA[N1 * COLS], bufB[N1 * COLS], oms[N1], twb[N2];
   const int f = blockIdx.y;
   const int n2_0 = blockIdx.x * COLS;
   for (int q = threadIdx.x; q < N1; q += NT) oms[q] = om1[q];
+  // four-step twiddle W^{k1 n2} (W = e^{-2 pi i / (N1 N2)}) with k1 n2 = N2 a + b: W_{N1}^{a} W^{b}, i.e.
+  // the N1 roots (oms) times row k1 = 1 of the tw1 table (W^{b}, b < N2)
+  const double2* tw1 = (const double2*)c.tw1;
+  for (int q = threadIdx.x; q < N2; q += NT) twb[q] = tw1[N2 + q];
   const FrameDesc fd = frames[f];
   const int N = c.N;
   const int64_t t0 = (int64_t)fd.k * c.hop - c.ext;
@@ -444,14 +448,15 @@ __global__ __launch_bounds__(256) void frames_dft1_c_kernel(DevConsts c, const v
   }
   __syncthreads();
   const double2* res = DctRadices1<N1>::template run<COLS, NT>(bufA, bufB, oms);
-  const double2* tw1 = (const double2*)c.tw1;
 #pragma unroll
   for (int it = 0; it < (TOT + NT - 1) / NT; ++it) {
     const int e = (int)threadIdx.x + it * NT;
     if (TOT % NT != 0 && e >= TOT) break;
     const int col = e % COLS, k1 = e / COLS;
     const int n2 = n2_0 + col;
-    z[((int64_t)f * N1 + k1) * N2 + n2] = cmul(res[k1 * COLS + col], tw1[k1 * N2 + n2]);
+    const int q = k1 * n2;  // < N1 N2
+    const double2 tw = cmul(oms[q / N2], twb[q % N2]);
+    z[((int64_t)f * N1 + k1) * N2 + n2] = cmul(res[k1 * COLS + col], tw);
   }
 }
 
