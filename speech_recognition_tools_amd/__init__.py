@@ -7,5 +7,6 @@ importing this package fails loudly when that library is missing.
 from ._lib import FdlpError, lib  # noqa: F401
 from .plan import DEFAULT_SUPPORT_EPS, FdlpPlan, FeatureConfig  # noqa: F401
 from .rng import NpRandom, PyRandom  # noqa: F401
+from . import ops  # noqa: F401,E402  (registers torch.ops.fdlp.spectrogram)
 
 __all__ = ["FdlpPlan", "FeatureConfig", "PyRandom", "NpRandom", "FdlpError", "DEFAULT_SUPPORT_EPS"]

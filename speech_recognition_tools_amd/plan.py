@@ -135,6 +135,14 @@ class FdlpPlan:
         check(lib.fdlp_plan_out_dim(h, ctypes.byref(d)))
         self.out_dim = d.value  # nfilters, or nfilters * feat_len in the modspec mode
 
+    @property
+    def op_id(self) -> int:
+        """Id of this plan for the torch.ops.fdlp.spectrogram operator (speech_recognition_tools_amd.ops)."""
+        if getattr(self, "_op_id", None) is None:
+            from .ops import register_plan
+            self._op_id = register_plan(self)
+        return self._op_id
+
     def close(self):
         h = getattr(self, "_h", None)
         if h:

@@ -293,3 +293,21 @@ def test_librispeech_scale_lengths_vs_oracle():
         got = out64[rows[i]:rows[i + 1]]
         assert got.shape == ref[u].shape, u
         assert np.abs(got - ref[u]).max() <= TOL, (u, lens[i], np.abs(got - ref[u]).max())
+
+
+def test_torch_op_matches_plan_compute():
+    """torch.ops.fdlp.spectrogram (the PyTorch-ROCm operator over fdlp_compute) == FdlpPlan.compute."""
+    from speech_recognition_tools_amd import FdlpPlan, FeatureConfig, PyRandom
+    meta, sig, ref, z = load_golden("wsj")
+    utts = meta["utts"]
+    lens = [sig[u].size for u in utts]
+    pcm = torch.from_numpy(np.concatenate([sig[u] for u in utts])).cuda()
+    plan = FdlpPlan(FeatureConfig.wsj(), device=0, max_frames=256)
+    nj = sum(plan.geometry(T)[0] - 1 for T in lens)
+    jit = PyRandom(meta["seed"]).randbits2(nj)
+    got = torch.ops.fdlp.spectrogram(plan.op_id, pcm, torch.tensor(lens, dtype=torch.int64),
+                                     torch.from_numpy(jit), 3)
+    want, rows, _ = plan.compute(pcm, lens, jit)
+    torch.cuda.synchronize()
+    assert got.shape == (int(rows[-1]), 80) and got.dtype == torch.float32
+    assert torch.equal(got, want)

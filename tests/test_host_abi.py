@@ -336,3 +336,11 @@ def test_structured_regions_match_filterbank_branches(fb):
         assert m2[j] == m1[j] + mid.sum() and mid[m1[j]:m2[j]].all()
     with pytest.raises(Exception):
         _host_plan(FeatureConfig()).regions()
+
+
+def test_torch_op_is_registered():
+    """torch.ops.fdlp.spectrogram (speech_recognition_tools_amd.ops) wraps fdlp_compute on tensors."""
+    import torch
+    import speech_recognition_tools_amd  # noqa: F401
+    schema = str(torch.ops.fdlp.spectrogram.default._schema)
+    assert schema.startswith("fdlp::spectrogram(") and "Tensor pcm" in schema and schema.endswith("-> Tensor")
