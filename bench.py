@@ -294,9 +294,11 @@ def main():
             dist.destroy_process_group()
         return
 
-    dev = torch.device("cuda", local)
+    # one rank per GPU; more ranks than visible GPUs share them round-robin (a correctness check of the
+    # N > 1 path on a small box, not a scaling measurement)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
-    plan = FdlpPlan(cfg, device=local, max_frames=frames)
+    plan = FdlpPlan(cfg, device=dev.index, max_frames=frames)
     if args.pipeline is not None:
         plan.set_pipeline(args.pipeline)
     _, lo, hi = probe.fbank()

@@ -13,7 +13,8 @@
 
 int main(int argc, char** argv) {
   const int items = argc > 1 ? atoi(argv[1]) : 327680;
-  const int p = 150, nlags = 152, M = 100, kk = 150, env_nfft = 300;
+  const int M = argc > 2 ? atoi(argv[2]) : 100;  // coeff_num: 100 (WSJ / CHiME-4), 450 (REVERB)
+  const int p = 150, nlags = 152, kk = 150, env_nfft = 300;
   std::vector<double> r((size_t)items * nlags);
   for (int it = 0; it < items; ++it) {
     // AR(2) autocorrelation with a per-item pole: r_l = rho^l cos(w l), plus a white floor
@@ -38,7 +39,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(d_cos, cosv.data(), cosv.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_win, win.data(), win.size() * 8, hipMemcpyHostToDevice));
   fdlp::DevConsts c{};
-  c.p = p; c.nlags = nlags; c.M = M; c.Me = M; c.kk = kk; c.env_nfft = env_nfft;
+  c.p = p; c.nlags = nlags; c.M = M; c.Me = M < env_nfft ? M : env_nfft; c.kk = kk; c.env_nfft = env_nfft;
   c.weights = d_w; c.env_cos = d_cos; c.env_win = d_win;
   CK(fdlp::prepare_lpc_env(c));  // lattice kernel launch geometry (FDLP_LPC_SLOTMAJOR / FDLP_LPC_LDS read here)
   hipStream_t s;
@@ -59,6 +60,6 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(env.data(), d_env, env.size() * 8, hipMemcpyDeviceToHost));
   double cs = 0;
   for (double v : env) cs += v;
-  printf("lpc_env phases=%d items=%d: %.4f ms/launch (checksum %.6e)\n", FDLP_LPC_PHASES, items, ms / reps, cs);
+  printf("lpc_env phases=%d items=%d M=%d: %.4f ms/launch (checksum %.6e)\n", FDLP_LPC_PHASES, items, M, ms / reps, cs);
   return 0;
 }

@@ -1803,6 +1803,7 @@ __global__ __launch_bounds__(64) void cepstrum_kernel(int p, int M, const double
 // -----------------------------------------------------------------------------------------
 struct LpcEnvArgs {
   int p, nlags, M, Me, kk, env_nfft, odd_zero, items, region;
+  int la_len;             // lattice kernel with a register cepstrum: doubles of the a area (cs follows, Me long)
   const double* r;
   const double* weights;  // [3, M]
   const double* env_cos;  // [env_nfft]
@@ -1852,21 +1853,48 @@ __device__ __forceinline__ double durbin16(double* la, const double* lr, int p, 
   return lr[0] + row_sum16(part);
 }
 
+// 16 finished-block terms of the cepstrum: acc += (k c_k from lane j) * alpha_{n-k} (alpha_{n-k} = al[-j]).
+// The 16 LDS values are loaded first: the FMAs are inline asm, which the scheduler does not move loads
+// across, so loads interleaved with them would each wait out their full LDS latency.
+__device__ __forceinline__ void cep_terms16(double& a0, double& a1, double& a2, double& a3, double kc,
+                                            const double* al) {
+  double v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = al[-j];
+  fmac_bcast<0>(a0, kc, v[0]);
+  fmac_bcast<1>(a1, kc, v[1]);
+  fmac_bcast<2>(a2, kc, v[2]);
+  fmac_bcast<3>(a3, kc, v[3]);
+  fmac_bcast<4>(a0, kc, v[4]);
+  fmac_bcast<5>(a1, kc, v[5]);
+  fmac_bcast<6>(a2, kc, v[6]);
+  fmac_bcast<7>(a3, kc, v[7]);
+  fmac_bcast<8>(a0, kc, v[8]);
+  fmac_bcast<9>(a1, kc, v[9]);
+  fmac_bcast<10>(a2, kc, v[10]);
+  fmac_bcast<11>(a3, kc, v[11]);
+  fmac_bcast<12>(a0, kc, v[12]);
+  fmac_bcast<13>(a1, kc, v[13]);
+  fmac_bcast<14>(a2, kc, v[14]);
+  fmac_bcast<15>(a3, kc, v[15]);
+}
+
 // In-block part of the cepstrum recurrence for coefficient b0 + KK: lane KK finishes c_{b0+KK},
 // DPP row_newbcast hands it to the row, the later lanes of the block fold it in.
+// a_kg is read from la only up to amax (beyond it a is zero: the reference pads alpha with zeros).
 template <int KK>
 __device__ __forceinline__ void cep_block_step(int b0, int M, int l, double gg, double inv_n, const double* la,
-                                               int n, double& acc, double& mine) {
+                                               int n, double& acc, double& mine, int amax = 1 << 30) {
   const int kg = b0 + KK;
   if (kg >= M) return;
   if (l == KK) {
     if (kg == 0) mine = log(sqrt(gg));
     else if (kg == 1) mine = -la[1];
-    else mine = -la[kg] - acc * inv_n;
+    else mine = -(kg <= amax ? la[kg] : 0.0) - acc * inv_n;
   }
   const double ck = dpp_f64<0x150 + KK>(mine);  // row_newbcast:KK
   if (kg >= 1 && l > KK) acc = fma((double)kg * ck, la[n - kg], acc);
-  if constexpr (KK + 1 < 16) cep_block_step<KK + 1>(b0, M, l, gg, inv_n, la, n, acc, mine);
+  if constexpr (KK + 1 < 16) cep_block_step<KK + 1>(b0, M, l, gg, inv_n, la, n, acc, mine, amax);
 }
 
 #ifndef FDLP_LPC_PHASES
@@ -2038,7 +2066,8 @@ constexpr int kEnvChunk = 5;  // envelope slots held in registers at a time
 // CB > 0 (M <= 16 CB): the cepstrum's finished blocks take c_k from the registers of the lane that
 // computed it (v_fmac_f64_dpp row_newbcast, the broadcast is the FMA's source modifier) instead of an
 // LDS read per term: one LDS read (alpha_{n-k}) and one FMA per term instead of two reads, a multiply
-// and an FMA.  CB = 0: the LDS form for any M.
+// and an FMA.  CB < 0: the same over a sliding register window of the last SL + 1 finished blocks
+// (any M; the terms with n - k > p are zero).  CB = 0: the LDS form for any M.
 // CONTIG: the contiguous-chunk Durbin (contig_durbin, default); otherwise the slot-major lattice
 // (lattice_durbin, FDLP_LPC_SLOTMAJOR=1).
 template <int SL, int CB = 0, bool CONTIG = true>
@@ -2071,9 +2100,14 @@ __global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(Lpc
     const int g = tid >> 4;
     const int l = tid & 15;
     const bool lane0 = l == 0;
-    const int NAL = (M > p + 1 ? M : p + 1) + 16;
-    double* la = sh + g * A.region;  // a_0..a_p, zeros up to NAL
-    double* cs = la + NAL;           // c_0..c_{M-1}
+    // LDS per item: la = a_0..a_p and zeros, then cs = the cepstrum.  The register cepstra (CB != 0)
+    // read la only below la_len and keep only the Me coefficients the envelope uses (compact: REVERB's
+    // M = 450 would otherwise cut the occupancy to one wave per SIMD); the LDS cepstrum (CB == 0) reads
+    // a and c up to M.
+    const int NAL = CB != 0 ? A.la_len : (M > p + 1 ? M : p + 1) + 16;
+    double* la = sh + g * A.region;
+    double* cs = la + NAL;
+    const int CSN = CB != 0 ? A.Me : M;  // coefficients kept in cs
     const int H = A.env_nfft >> 1;
     const int TS = (A.env_nfft / 4 + 1 + 15) / 16;
     const int item = grp * 4 + g;
@@ -2139,31 +2173,69 @@ __global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(Lpc
 #pragma unroll
         for (int bp = 0; bp < b; ++bp) {
           const double* al = la + n - 16 * bp;  // alpha_{n - k} = la[n - k], k = 16 bp + j
-          fmac_bcast<0>(a0, kc[bp], al[0]);
-          fmac_bcast<1>(a1, kc[bp], al[-1]);
-          fmac_bcast<2>(a2, kc[bp], al[-2]);
-          fmac_bcast<3>(a3, kc[bp], al[-3]);
-          fmac_bcast<4>(a0, kc[bp], al[-4]);
-          fmac_bcast<5>(a1, kc[bp], al[-5]);
-          fmac_bcast<6>(a2, kc[bp], al[-6]);
-          fmac_bcast<7>(a3, kc[bp], al[-7]);
-          fmac_bcast<8>(a0, kc[bp], al[-8]);
-          fmac_bcast<9>(a1, kc[bp], al[-9]);
-          fmac_bcast<10>(a2, kc[bp], al[-10]);
-          fmac_bcast<11>(a3, kc[bp], al[-11]);
-          fmac_bcast<12>(a0, kc[bp], al[-12]);
-          fmac_bcast<13>(a1, kc[bp], al[-13]);
-          fmac_bcast<14>(a2, kc[bp], al[-14]);
-          fmac_bcast<15>(a3, kc[bp], al[-15]);
+          cep_terms16(a0, a1, a2, a3, kc[bp], al);
         }
         double acc = (a0 + a1) + (a2 + a3);
         double mine = 0.0;
-        cep_block_step<0>(b0, M, l, gg, inv_n, la, n, acc, mine);
+        cep_block_step<0>(b0, M, l, gg, inv_n, la, n, acc, mine, p);
         kc[b] = n == 0 ? 0.0 : (double)n * mine;
-        if (n < M) {
-          cs[n] = mine;
-          if (valid && A.cep_out) A.cep_out[(int64_t)item * M + n] = mine;
+        if (n < CSN) cs[n] = mine;
+        if (n < M && valid && A.cep_out) A.cep_out[(int64_t)item * M + n] = mine;
+      }
+      wave_lds_sync();
+    } else if constexpr (CB < 0) {
+      // any M (REVERB: 450): the same register broadcast over a sliding window of the last W finished
+      // blocks.  alpha_{n-k} = 0 for n - k > p, and the window covers every k >= b0 - 16 W <= n - p, so
+      // the terms it adds beyond the reference's range are exact zeros (la is zero past p).
+      constexpr int W = SL;  // block w holds n - k >= 16 w + 1; w >= ceil(p / 16) <= SL is all zero terms
+      double kc[W];              // kc[w]: n c_n (lane l) of block b - 1 - w; 0 before block 0
+#pragma unroll
+      for (int w = 0; w < W; ++w) kc[w] = 0.0;
+      // only c_0 .. c_{Me-1} reach the envelope (fft(., env_nfft) truncates, :201); all M are computed
+      // when the cepstra themselves are an output (debug / modulation-spectrum mode)
+      const int Mc = A.cep_out ? M : A.Me;
+      for (int b0 = 0; b0 < ((FDLP_LPC_PHASES & 2) ? Mc : 0); b0 += 16) {
+        const int n = b0 + l;
+        const double inv_n = 1.0 / (double)(n > 0 ? n : 1);
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        asm volatile("s_nop 1");  // kc[0] was just written: DPP reads need 2 wait states
+        // the next block-term's 16 alpha values are loaded before this one's FMAs (double buffer)
+        double v[2][16];
+        const double* al0 = la + n - b0 + 16;  // k = b0 - 16 (w + 1) + j: alpha_{n-k} = al0[16 w - j]
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[0][j] = al0[-j];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          if (w + 1 < W) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[(w + 1) & 1][j] = al0[16 * (w + 1) - j];
+          }
+          const double* vv = v[w & 1];
+          fmac_bcast<0>(a0, kc[w], vv[0]);
+          fmac_bcast<1>(a1, kc[w], vv[1]);
+          fmac_bcast<2>(a2, kc[w], vv[2]);
+          fmac_bcast<3>(a3, kc[w], vv[3]);
+          fmac_bcast<4>(a0, kc[w], vv[4]);
+          fmac_bcast<5>(a1, kc[w], vv[5]);
+          fmac_bcast<6>(a2, kc[w], vv[6]);
+          fmac_bcast<7>(a3, kc[w], vv[7]);
+          fmac_bcast<8>(a0, kc[w], vv[8]);
+          fmac_bcast<9>(a1, kc[w], vv[9]);
+          fmac_bcast<10>(a2, kc[w], vv[10]);
+          fmac_bcast<11>(a3, kc[w], vv[11]);
+          fmac_bcast<12>(a0, kc[w], vv[12]);
+          fmac_bcast<13>(a1, kc[w], vv[13]);
+          fmac_bcast<14>(a2, kc[w], vv[14]);
+          fmac_bcast<15>(a3, kc[w], vv[15]);
         }
+        double acc = (a0 + a1) + (a2 + a3);
+        double mine = 0.0;
+        cep_block_step<0>(b0, Mc, l, gg, inv_n, la, n, acc, mine, p);
+#pragma unroll
+        for (int w = W - 1; w > 0; --w) kc[w] = kc[w - 1];
+        kc[0] = n == 0 ? 0.0 : (double)n * mine;
+        if (n < CSN) cs[n] = mine;
+        if (n < M && valid && A.cep_out) A.cep_out[(int64_t)item * M + n] = mine;
       }
       wave_lds_sync();
     }
@@ -2192,7 +2264,7 @@ __global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(Lpc
       wave_lds_sync();
     }
     // ---- phase 3: weights + envelope (computeFDLPSpectrogram.py:194-205) ---------------------
-    double* cw = la;
+    double* cw = CB != 0 ? cs : la;  // compact layout: weighted in place
     const double* mask = A.weights;
     const double* lif = A.weights + M;
     const double* gam = A.weights + 2 * M;
@@ -2707,6 +2779,14 @@ static hipError_t lattice_dispatch_sl(const DevConsts& c, Fn&& fn) {
       default: break;
     }
   }
+  if (!c.lpc_cep_lds && c.M > 16 * 7 && SL >= 9 && SL <= 11) {  // the same over a sliding window (REVERB: M 450)
+    switch (SL) {
+      case 9: return fn(integral_constant<int, 9>{}, integral_constant<int, -1>{});
+      case 10: return fn(integral_constant<int, 10>{}, integral_constant<int, -1>{});
+      case 11: return fn(integral_constant<int, 11>{}, integral_constant<int, -1>{});
+      default: break;
+    }
+  }
   switch (SL) {
 #define FDLP_SL_CASE(n) case n: return fn(integral_constant<int, n>{}, integral_constant<int, 0>{});
     FDLP_SL_CASE(1) FDLP_SL_CASE(2) FDLP_SL_CASE(3) FDLP_SL_CASE(4) FDLP_SL_CASE(5) FDLP_SL_CASE(6)
@@ -2727,10 +2807,20 @@ static hipError_t lattice_dispatch(const DevConsts& c, Fn&& fn) {
   });
 }
 
-static size_t lattice_lds(const DevConsts& c) {
-  const int NAL = (c.M > c.p + 1 ? c.M : c.p + 1) + 16;
-  const int region = (NAL + c.M + 15) / 32 * 32 + 16;  // = 16 mod 32 doubles (disjoint bank halves per item)
-  return sizeof(double) * 4 * (size_t)region;
+// a-area length of the compact layout (register cepstra, CB != 0): the Durbin writes 16 SL positions,
+// CB > 0 reads a below 16 CB, the window (CB < 0, W = SL blocks) below 16 SL + 16
+static int lattice_la_len(const DevConsts& c, int CB, int SL) {
+  int la = std::max(c.p + 2, 16 * SL);
+  if (CB > 0) la = std::max(la, 16 * CB);
+  if (CB < 0) la = std::max(la, 16 * SL + 16);
+  return la;
+}
+static int lattice_region(const DevConsts& c, int CB, int SL) {
+  const int need = CB != 0 ? lattice_la_len(c, CB, SL) + c.Me : (c.M > c.p + 1 ? c.M : c.p + 1) + 16 + c.M;
+  return (need + 15) / 32 * 32 + 16;  // = 16 mod 32 doubles (disjoint bank halves per item)
+}
+static size_t lattice_lds(const DevConsts& c, int CB, int SL) {
+  return sizeof(double) * 4 * (size_t)lattice_region(c, CB, SL);
 }
 
 hipError_t prepare_lpc_env(DevConsts& c) {
@@ -2742,11 +2832,11 @@ hipError_t prepare_lpc_env(DevConsts& c) {
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
-  const size_t lds = lattice_lds(c);
   int per_cu = 0;
   e = lattice_dispatch(c, [&](auto sl, auto cb, auto ct) -> hipError_t {
     constexpr int SL = decltype(sl)::value, CB = decltype(cb)::value;
     constexpr bool CT = decltype(ct)::value;
+    const size_t lds = lattice_lds(c, CB, SL);
     if (lds > 65536) {
       const hipError_t a = hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL, CB, CT>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -2765,16 +2855,17 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
   if (items <= 0) return hipSuccess;
   LpcEnvArgs A;
   A.p = c.p; A.nlags = c.nlags; A.M = c.M; A.Me = c.Me; A.kk = c.kk; A.env_nfft = c.env_nfft;
-  A.odd_zero = odd_zero; A.items = items; A.region = lpc_env_region(c.p, c.M);
+  A.odd_zero = odd_zero; A.items = items; A.region = lpc_env_region(c.p, c.M); A.la_len = 0;
   A.r = r; A.weights = c.weights; A.env_cos = c.env_cos; A.env_win = c.env_win; A.env = env;
   A.a_out = a_out; A.gg_out = gg_out; A.cep_out = cep_out;
   if (c.lpc_blocks > 0) {  // lattice Durbin in registers, persistent grid (prepare_lpc_env)
-    const size_t lds = lattice_lds(c);
-    A.region = (int)(lds / (4 * sizeof(double)));
     const int grid = std::min((items + 3) / 4, c.lpc_blocks);
     return lattice_dispatch(c, [&](auto sl, auto cb, auto ct) -> hipError_t {
       constexpr int SL = decltype(sl)::value, CB = decltype(cb)::value;
       constexpr bool CT = decltype(ct)::value;
+      const size_t lds = lattice_lds(c, CB, SL);
+      A.region = lattice_region(c, CB, SL);
+      A.la_len = CB != 0 ? lattice_la_len(c, CB, SL) : 0;
       hipLaunchKernelGGL((lpc_env_lattice_kernel<SL, CB, CT>), dim3(grid), dim3(64), lds, s, A);
       return hipGetLastError();
     });
