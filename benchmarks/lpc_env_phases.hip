@@ -34,6 +34,9 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&d_cos, cosv.size() * 8));
   CK(hipMalloc(&d_win, win.size() * 8));
   CK(hipMalloc(&d_env, (size_t)items * kk * 8));
+  double *d_a, *d_gg;  // split Durbin workspace (durbin8_kernel)
+  CK(hipMalloc(&d_a, (size_t)items * (p + 1) * 8));
+  CK(hipMalloc(&d_gg, (size_t)items * 8));
   CK(hipMemcpy(d_r, r.data(), r.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_w, weights.data(), weights.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_cos, cosv.data(), cosv.size() * 8, hipMemcpyHostToDevice));
@@ -44,14 +47,14 @@ int main(int argc, char** argv) {
   CK(fdlp::prepare_lpc_env(c));  // lattice kernel launch geometry (FDLP_LPC_SLOTMAJOR / FDLP_LPC_LDS read here)
   hipStream_t s;
   CK(hipStreamCreate(&s));
-  for (int i = 0; i < 3; ++i) CK(fdlp::launch_lpc_env(c, 0, d_r, items, d_env, nullptr, nullptr, nullptr, s));
+  for (int i = 0; i < 3; ++i) CK(fdlp::launch_lpc_env(c, 0, d_r, items, d_env, nullptr, nullptr, nullptr, d_a, d_gg, s));
   CK(hipStreamSynchronize(s));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int reps = 20;
   CK(hipEventRecord(e0, s));
-  for (int i = 0; i < reps; ++i) CK(fdlp::launch_lpc_env(c, 0, d_r, items, d_env, nullptr, nullptr, nullptr, s));
+  for (int i = 0; i < reps; ++i) CK(fdlp::launch_lpc_env(c, 0, d_r, items, d_env, nullptr, nullptr, nullptr, d_a, d_gg, s));
   CK(hipEventRecord(e1, s));
   CK(hipEventSynchronize(e1));
   float ms = 0;

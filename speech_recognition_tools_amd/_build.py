@@ -29,15 +29,19 @@ def stale():
     return False
 
 
-def build(force=False, verbose=False):
-    if not force and not stale():
+def build(force=False, verbose=False, out=None, defines=()):
+    """out / defines: an A/B variant of the library (e.g. -DFDLP_D8_CHAINS=2) at another path, loaded
+    through FDLP_LIB; the default build is LIB."""
+    target = out or LIB
+    if not force and out is None and not stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(os.path.dirname(os.path.abspath(target)), exist_ok=True)
     objs = []
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function",
-             "-munsafe-fp-atomics"]
+             "-munsafe-fp-atomics"] + list(defines)
     for src in SOURCES:
-        obj = os.path.join(LIBDIR, src + ".o")
+        obj = os.path.join(LIBDIR, src + ".ab.o" if out else src + ".o")
         lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "c++"]
         cmd = [hipcc()] + flags + lang + ["-c", os.path.join(CSRC, src), "-o", obj]
         if src.endswith(".cpp"):
@@ -47,14 +51,18 @@ def build(force=False, verbose=False):
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = target + ".tmp"
     cmd = [hipcc(), "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", tmp] + objs
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, target)
     for o in objs:
         os.unlink(o)
-    return LIB
+    return target
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    # python _build.py [--force] [--out PATH -DNAME=VALUE ...]
+    argv = sys.argv[1:]
+    out = argv[argv.index("--out") + 1] if "--out" in argv else None
+    defs = [a for a in argv if a.startswith("-D")]
+    print(build(force="--force" in argv, verbose=True, out=out, defines=defs))

@@ -87,6 +87,8 @@ struct DevConsts {
   int lpc_lds_durbin = 0;  // FDLP_LPC_LDS at plan creation: the LDS Durbin instead of the lattice
   int lpc_cep_lds = 0;     // FDLP_CEP_LDS at plan creation: the LDS cepstrum form for every M
   int lpc_slotmajor = 0;   // FDLP_LPC_SLOTMAJOR at plan creation: the slot-major lattice Durbin
+  int lpc_split = 0;       // the Durbin as durbin8_kernel (8 lanes per item), then the cepstrum/envelope
+                           // kernel; off with FDLP_LPC_FUSED=1 (set by prepare_lpc_env)
   int dct_generic = 0;     // FDLP_DCT_GENERIC at plan creation: runtime-radix DCT passes for every N
 };
 
@@ -120,8 +122,10 @@ hipError_t launch_levinson(const DevConsts& c, const double* r, int items, doubl
                            double* gg, hipStream_t s);
 hipError_t launch_cepstrum(int p, int M, const double* a, const double* gg, int items,
                            double* cep, hipStream_t s);
+// a_ws / gg_ws: [items, p+1] / [items] workspace of the split Durbin (durbin8_kernel, c.lpc_split)
 hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int items, double* env,
-                          double* a_out, double* gg_out, double* cep_out, hipStream_t s);
+                          double* a_out, double* gg_out, double* cep_out, double* a_ws, double* gg_ws,
+                          hipStream_t s);
 int lpc_env_region(int p, int M);
 // Per-plan launch setup of launch_lpc_env for the current device: sets the kernel's large-LDS
 // attribute and stores the resident block count in c.lpc_blocks.

@@ -305,6 +305,16 @@ __global__ __launch_bounds__(256) void dft2_dct_kernel(DevConsts c, DftPlan d2, 
   }
 }
 
+// Workgroup b is dispatched to XCD b % 8.  Giving every XCD a contiguous run of work items keeps
+// the items that read the same frame (its D row) on one L2 instead of pulling the row into all
+// eight.  Grid = 8 * ceil(total / 8); the padding workgroups get an index >= total.
+constexpr int kXcds = 8;
+__device__ __forceinline__ int xcd_item() {
+  const int per = gridDim.x / kXcds;
+  return (int)(blockIdx.x % kXcds) * per + (int)(blockIdx.x / kXcds);
+}
+static inline int xcd_grid(int total) { return (total + kXcds - 1) / kXcds * kXcds; }
+
 // -----------------------------------------------------------------------------------------
 // 1s/2s. The same two DCT passes specialised at compile time for the recipes' frame length
 // (N = 24000: packed length-12000 complex FFT = 100 x 120; radices 4.5.5 and 8.3.5): constant
@@ -411,11 +421,15 @@ __global__ __launch_bounds__(256) void frames_dft1_c_kernel(DevConsts c, const v
                                                             const int16_t* __restrict__ noise,
                                                             const FrameDesc* __restrict__ frames,
                                                             const double2* __restrict__ om1,
-                                                            double2* __restrict__ z) {
+                                                            double2* __restrict__ z, int nframes) {
   constexpr int NT = 256;
   __shared__ double2 bufA[N1 * COLS], bufB[N1 * COLS], oms[N1], twb[N2];
-  const int f = blockIdx.y;
-  const int n2_0 = blockIdx.x * COLS;
+  // 1-D grid, XCD-mapped: the column blocks of a frame run on one XCD (their z rows share L2 lines)
+  constexpr int NBX = (N2 + COLS - 1) / COLS;
+  const int it0 = xcd_item();
+  if (it0 >= nframes * NBX) return;
+  const int f = it0 / NBX;
+  const int n2_0 = (it0 - f * NBX) * COLS;
   for (int q = threadIdx.x; q < N1; q += NT) oms[q] = om1[q];
   // four-step twiddle W^{k1 n2} (W = e^{-2 pi i / (N1 N2)}) with k1 n2 = N2 a + b: W_{N1}^{a} W^{b}, i.e.
   // the N1 roots (oms) times row k1 = 1 of the tw1 table (W^{b}, b < N2)
@@ -464,14 +478,20 @@ __global__ __launch_bounds__(256) void frames_dft1_c_kernel(DevConsts c, const v
 template <int N1, int N2, int COLS, bool TWF = true>
 __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const double2* __restrict__ z,
                                                          const double2* __restrict__ om2, double inv_scale_div,
-                                                         double* __restrict__ dct) {
+                                                         double* __restrict__ dct, int nframes) {
   constexpr int NT = 256, HALF = COLS / 2;
   __shared__ double2 bufA[N2 * COLS], bufB[N2 * COLS], oms[N2];
   __shared__ double2 pw1[N1], pw2[N2], rw1[N1], rw2[N2];  // factored twiddles (TWF)
-  const int f = blockIdx.y;
+  // 1-D grid, XCD-mapped: the row-pair blocks of a frame run on one XCD, so the 32-B runs they store
+  // into each D line (k = k1 + N1 k2: 4 consecutive k1 per block) merge in that XCD's L2
+  constexpr int NBX = (N1 / 2 + 1 + HALF - 1) / HALF;
+  const int it0 = xcd_item();
+  if (it0 >= nframes * NBX) return;
+  const int f = it0 / NBX;
+  const int bx = it0 - f * NBX;
   const int N = c.N;
   auto slot_row = [&](int r) -> int {
-    const int pp = blockIdx.x * HALF + (r % HALF);
+    const int pp = bx * HALF + (r % HALF);
     if (2 * pp > N1) return -1;
     if (r < HALF) return pp;
     const int m = N1 - pp;
@@ -881,16 +901,6 @@ __device__ __forceinline__ void diag_sums(const dbl4* acc, double* ep, int nlags
     __syncthreads();
   }
 }
-
-// Workgroup b is dispatched to XCD b % 8.  Giving every XCD a contiguous run of work items keeps
-// the items that read the same frame (its D row) on one L2 instead of pulling the row into all
-// eight.  Grid = 8 * ceil(total / 8); the padding workgroups get an index >= total.
-constexpr int kXcds = 8;
-__device__ __forceinline__ int xcd_item() {
-  const int per = gridDim.x / kXcds;
-  return (int)(blockIdx.x % kXcds) * per + (int)(blockIdx.x / kXcds);
-}
-static inline int xcd_grid(int total) { return (total + kXcds - 1) / kXcds * kXcds; }
 
 // Diagonal sums in lag blocks of LB lags (LB = 32 or 64), branch-free.  Block g covers lags
 // [LB g, LB g + LB); its 16-term sums touch tiles LB/16 g .. LB/16 (g+1), which are written whole
@@ -1812,6 +1822,8 @@ struct LpcEnvArgs {
   double* a_out;          // nullable [items, p+1]
   double* gg_out;         // nullable [items]
   double* cep_out;        // nullable [items, M]
+  const double* a_ext;    // DM = 2: a [items, p+1] and gg [items] from durbin8_kernel
+  const double* gg_ext;
 };
 
 // Durbin recursion with a[] resident in LDS (la[0..p], zero beyond) and r in LDS (lr): lane l of
@@ -2060,6 +2072,155 @@ __device__ __forceinline__ void contig_durbin(double (&A)[S], double (&B)[S], do
   for (int j = 0; j < S; ++j) la[l * S + j] = A[j];
 }
 
+// -----------------------------------------------------------------------------------------
+// The contiguous-chunk lattice Durbin with 8 lanes per item (each half of a DPP row is an item, 8 items
+// per wave).  Per order the cross-lane part (the 8-lane sum, 1/E by rcp + two Newton steps, kappa, the
+// E update: ~20 VALU instructions) is paid once for 8 items instead of 4, and the FMAs (3 per position)
+// are the same, so the Durbin issues ~35 % fewer instructions per item than contig_durbin (p = 150).
+// In phase S lane li (0..7) owns positions li S .. li S + S - 1 (capacity 8 S, orders < 8 S); the shift
+// z B takes lane li - 1's last slot by row_shr:1, which would carry lane 7 of the first item into lane 8
+// of the second: the first lane of each item takes 0 instead (a select).  Standalone kernel
+// (durbin8_kernel): a [items, p + 1] and gg go to global memory for lpc_env_lattice_kernel's cepstrum and
+// envelope phases (DM = 2), which then run at their own occupancy.  Same recursion as contig_step
+// (features.py:226-228); only the summation order of the order-k dot product differs (8 lane partials).
+// -----------------------------------------------------------------------------------------
+#ifndef FDLP_D8_CHAINS
+#define FDLP_D8_CHAINS 4  // 2 or 4
+#endif
+template <int S>
+__device__ __forceinline__ void c8_step(double (&A)[S], const double (&Bs)[S], double (&Bd)[S],
+                                        const double (&R1)[S], double& part, double& E, bool first) {
+  const double acc = sum8(part);  // r_k + sum_i a_i r_{k-i}
+  double rE = __builtin_amdgcn_rcp(E);
+  rE = fma(rE, fma(-E, rE, 1.0), rE);
+  rE = fma(rE, fma(-E, rE, 1.0), rE);
+  const double kappa = -acc * rE;
+  const double zs = __builtin_amdgcn_update_dpp(0.0, Bs[S - 1], 0x111, 0xF, 0xF, true);  // row_shr:1
+  const double z0 = first ? 0.0 : zs;
+  // the next order's dot product in D independent chains (the chain, not the issue, bounds small S)
+  constexpr int D = FDLP_D8_CHAINS;
+  double pc[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) pc[d] = 0.0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const double zb = j == 0 ? z0 : Bs[j - 1];
+    Bd[j] = fma(kappa, A[j], zb);
+    A[j] = fma(kappa, zb, A[j]);
+    pc[j % D] = fma(Bd[j], R1[j], pc[j % D]);
+  }
+  if constexpr (D == 4) part = (pc[0] + pc[1]) + (pc[2] + pc[3]);
+  else part = pc[0] + pc[1];
+  E = E * (1.0 - kappa * kappa);
+}
+
+// R1 of phase S for lane li from the item's staged r (rl[m] = r_{m+1}, 0 past p)
+template <int S>
+__device__ __forceinline__ void c8_load_r1(double (&R1)[S], const double* rl, int li) {
+#pragma unroll
+  for (int j = 0; j < S; ++j) R1[j] = rl[li * S + j];
+}
+
+// A (S per lane) -> sc -> An, Bn (S + 1 per lane).  B is the bitwise mirror of A: after order 8 S - 1,
+// b_m = a_{8S-1-m} (both are fma(kappa, a_m, a_{k-m}) in c8_step), so B is read back mirrored from A's
+// image instead of being written too; sc[8 S ..] and sc[-8 .. -1] are zeros (positions >= 8 S).
+template <int S>
+__device__ __forceinline__ void c8_relayout(const double (&A)[S], double (&An)[S + 1], double (&Bn)[S + 1],
+                                            double* sc, int li) {
+  wave_lds_sync();
+#pragma unroll
+  for (int j = 0; j < S; ++j) sc[li * S + j] = A[j];
+  sc[8 * S + li] = 0.0;
+  wave_lds_sync();
+#pragma unroll
+  for (int j = 0; j <= S; ++j) An[j] = sc[li * (S + 1) + j];
+#pragma unroll
+  for (int j = 0; j <= S; ++j) Bn[j] = sc[8 * S - 1 - li * (S + 1) - j];
+}
+
+template <int SL8, int S>
+__device__ __forceinline__ void c8_durbin(double (&A)[S], double (&B)[S], double (&R1)[S], double& part, double& E,
+                                          const double* rl, double* sc, int p, int li, bool valid, double r0,
+                                          double* ao, double* go) {
+  const int k0 = S == 1 ? 1 : 8 * (S - 1);
+  const int k1 = min(p + 1, 8 * S);
+  const bool first = li == 0;
+  constexpr int SN = S < SL8 ? S + 1 : S;
+  double R1n[SN];
+  if constexpr (S < SL8) {
+    if (k1 <= p) c8_load_r1<SN>(R1n, rl, li);  // next phase's R1 (LDS), consumed after the loop
+  }
+  double B2[S];
+  int k = k0;
+  for (; k + 1 < k1; k += 2) {
+    c8_step<S>(A, B, B2, R1, part, E, first);
+    c8_step<S>(A, B2, B, R1, part, E, first);
+  }
+  if (k < k1) {
+    c8_step<S>(A, B, B2, R1, part, E, first);
+#pragma unroll
+    for (int j = 0; j < S; ++j) B[j] = B2[j];
+  }
+  if constexpr (S < SL8) {
+    if (k1 <= p) {
+      double An[S + 1], Bn[S + 1];
+      c8_relayout<S>(A, An, Bn, sc, li);
+      c8_durbin<SL8, S + 1>(An, Bn, R1n, part, E, rl, sc, p, li, valid, r0, ao, go);
+      return;
+    }
+  }
+  // order p done: gg = r0 + sum_{m=0}^{p} a_m r_{m+1} (the reference's off-by-one, features.py:228)
+  double q0 = 0.0, q1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    if (j & 1) q1 = fma(A[j], R1[j], q1);
+    else q0 = fma(A[j], R1[j], q0);
+  }
+  const double gg = r0 + sum8(q0 + q1);
+  if (valid) {
+#pragma unroll
+    for (int j = 0; j < S; ++j)
+      if (li * S + j <= p) ao[li * S + j] = A[j];
+    if (first) *go = gg;
+  }
+}
+
+// one wave per 8 items (p + 1 <= 8 SL8); a / gg: [items, p + 1] / [items].  The 8 items' r rows are
+// staged in LDS first (one coalesced pass), so each phase's R1 is an LDS read, not a global load
+// whose latency the short early phases cannot cover.  LDS per item: r_1 .. r_{8 SL8} and the relayout
+// image (8 zeros + 8 SL8); 8 items = 19.5 KB at SL8 = 19, two waves per SIMD.
+template <int SL8>
+__global__ __launch_bounds__(64, 2) void durbin8_kernel(const double* __restrict__ r, int nlags, int p, int items,
+                                                        double* __restrict__ a, double* __restrict__ gg) {
+  constexpr int kR = 8 * SL8;
+  constexpr int kItem = kR + 8 + 8 * SL8;
+  __shared__ double lds[8 * kItem];
+  const int lane = threadIdx.x;
+  const int li = lane & 7;
+  const int ii = lane >> 3;
+  const int item0 = blockIdx.x * 8;
+  for (int q = lane; q < 8 * kR; q += 64) {
+    const int i = q / kR, m = q - i * kR;
+    const int itm = item0 + i;
+    double v = 0.0;
+    if (itm < items && m <= p && m + 1 < nlags) v = r[(int64_t)itm * nlags + m + 1];
+    lds[i * kItem + m] = v;
+  }
+  double* sc = lds + ii * kItem + kR + 8;
+  sc[li - 8] = 0.0;
+  wave_lds_sync();
+  const int item = item0 + ii;
+  const bool valid = item < items;
+  const double r0 = valid ? r[(int64_t)item * nlags] : 1.0;
+  const double* rl = lds + ii * kItem;
+  double A1[1] = {li == 0 ? 1.0 : 0.0}, B1[1] = {li == 0 ? 1.0 : 0.0}, R11[1];
+  c8_load_r1<1>(R11, rl, li);
+  double part = li == 0 ? R11[0] : 0.0;  // order 1: b^(0) . R1 = r_1
+  double E = r0;
+  c8_durbin<SL8, 1>(A1, B1, R11, part, E, rl, sc, p, li, valid, r0, a + (int64_t)(valid ? item : 0) * (p + 1),
+                    gg + (valid ? item : 0));
+}
+
 // lpc_env with the lattice Durbin: persistent waves (grid-stride over groups of 4 items), r read
 // straight into registers, LDS only for a (cepstrum) and c (envelope).  Same outputs as lpc_env_kernel.
 constexpr int kEnvChunk = 5;  // envelope slots held in registers at a time
@@ -2068,9 +2229,11 @@ constexpr int kEnvChunk = 5;  // envelope slots held in registers at a time
 // LDS read per term: one LDS read (alpha_{n-k}) and one FMA per term instead of two reads, a multiply
 // and an FMA.  CB < 0: the same over a sliding register window of the last SL + 1 finished blocks
 // (any M; the terms with n - k > p are zero).  CB = 0: the LDS form for any M.
-// CONTIG: the contiguous-chunk Durbin (contig_durbin, default); otherwise the slot-major lattice
-// (lattice_durbin, FDLP_LPC_SLOTMAJOR=1).
-template <int SL, int CB = 0, bool CONTIG = true>
+// DM: the Durbin phase.  1: the contiguous-chunk Durbin (contig_durbin); 0: the slot-major lattice
+// (lattice_durbin, FDLP_LPC_SLOTMAJOR=1); 2: none, a and gg come from durbin8_kernel (A.a_ext, A.gg_ext;
+// default where durbin8_kernel is instantiated).
+constexpr int kDmSlotMajor = 0, kDmContig = 1, kDmExt = 2;
+template <int SL, int CB = 0, int DM = kDmContig>
 #ifndef FDLP_LAT_WAVES
 #define FDLP_LAT_WAVES 4  // waves per SIMD the lattice kernel is compiled for (register budget)
 #endif
@@ -2080,15 +2243,16 @@ __global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(Lpc
   const int ngroups = (A.items + 3) >> 2;
   // (prefetching the next group's r into registers before the envelope phase was measured: no gain,
   // it costs a wave per SIMD of occupancy)
-  double Rn[CONTIG ? 1 : SL], r0n;
+  constexpr bool CONTIG = DM == kDmContig;
+  double Rn[DM == kDmSlotMajor ? SL : 1], r0n;
   auto load_r = [&](int grp) {
     const int it = grp * 4 + (threadIdx.x >> 4);
     const double* rr = A.r + (int64_t)(it < A.items ? it : 0) * A.nlags;
-    if constexpr (!CONTIG) {
+    if constexpr (DM == kDmSlotMajor) {
 #pragma unroll
       for (int s = 0; s < SL; ++s) Rn[s] = rr[min((int)(threadIdx.x & 15) + 16 * s + 1, A.nlags - 1)];
     }
-    r0n = rr[0];
+    if constexpr (DM != kDmExt) r0n = rr[0];
   };
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     load_r(grp);
@@ -2114,7 +2278,12 @@ __global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(Lpc
     const bool valid = item < A.items;
     // ---- phase 1: Levinson-Durbin (features.py:226-228) in registers -------------------------
     double gg;
-    if constexpr (CONTIG) {
+    if constexpr (DM == kDmExt) {
+      const double* ai = A.a_ext + (int64_t)(valid ? item : 0) * (p + 1);
+      wave_lds_sync();  // the previous group's envelope reads of la are done
+      for (int q = l; q < NAL; q += 16) la[q] = (valid && q <= p) ? ai[q] : 0.0;
+      gg = valid ? A.gg_ext[item] : 1.0;
+    } else if constexpr (CONTIG) {
       const double* rr = A.r + (int64_t)(valid ? item : 0) * A.nlags;
       const double r0 = valid ? r0n : 1.0;
       gg = r0;
@@ -2516,8 +2685,8 @@ hipError_t launch_frames_dft1(const DevConsts& c, const DftPlan& d1, int N2, con
   dim3 grid((N2 + kDftCols - 1) / kDftCols, nframes);
   size_t lds = sizeof(double2) * (2 * d1.n * kDftCols + d1.n);
   if (c.real_fft && !c.dct_generic && d1.n == 100 && N2 == 120 && !dense_rows) {  // recipes: N = 24000
-    hipLaunchKernelGGL((frames_dft1_c_kernel<100, 120, kDftCols>), grid, dim3(256), 0, s, c, pcm, pcm_kind, noise,
-                       frames, om1, z);
+    hipLaunchKernelGGL((frames_dft1_c_kernel<100, 120, kDftCols>), dim3(xcd_grid(grid.x * nframes)), dim3(256), 0, s, c,
+                       pcm, pcm_kind, noise, frames, om1, z, nframes);
     return hipGetLastError();
   }
   if (c.real_fft) {
@@ -2540,10 +2709,11 @@ hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const 
   if (c.real_fft && !c.dct_generic && N1 == 100 && d2.n == 120) {  // recipes: N = 24000
     dim3 grid((N1 / 2 + 1 + kDftCols / 2 - 1) / (kDftCols / 2), nframes);
     static const bool table_tw = getenv("FDLP_DCT_TABLE_TW") != nullptr;  // A/B knob: full post/rtw tables
+    const dim3 g1(xcd_grid(grid.x * nframes));
     if (table_tw)
-      hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, false>), grid, dim3(256), 0, s, c, z, om2, div, dct);
+      hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, false>), g1, dim3(256), 0, s, c, z, om2, div, dct, nframes);
     else
-      hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, true>), grid, dim3(256), 0, s, c, z, om2, div, dct);
+      hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, true>), g1, dim3(256), 0, s, c, z, om2, div, dct, nframes);
     return hipGetLastError();
   }
   if (c.real_fft) {
@@ -2797,13 +2967,33 @@ static hipError_t lattice_dispatch_sl(const DevConsts& c, Fn&& fn) {
   }
 }
 
-// fn(integral_constant<SL>, integral_constant<CB>, integral_constant<bool, CONTIG>)
+// durbin8_kernel instantiations: 8 SL8 >= p + 1 for the lattice range SL = 9..11 (p 128..175)
+static bool durbin8_fits(int p) {
+  const int sl8 = (p + 1 + 7) / 8;
+  return sl8 >= 17 && sl8 <= 22;
+}
+template <class Fn>
+static hipError_t durbin8_dispatch(int p, Fn&& fn) {
+  using std::integral_constant;
+  switch ((p + 1 + 7) / 8) {
+    case 17: return fn(integral_constant<int, 17>{});
+    case 18: return fn(integral_constant<int, 18>{});
+    case 19: return fn(integral_constant<int, 19>{});
+    case 20: return fn(integral_constant<int, 20>{});
+    case 21: return fn(integral_constant<int, 21>{});
+    case 22: return fn(integral_constant<int, 22>{});
+    default: return hipErrorNotSupported;
+  }
+}
+
+// fn(integral_constant<SL>, integral_constant<CB>, integral_constant<int, DM>)
 template <class Fn>
 static hipError_t lattice_dispatch(const DevConsts& c, Fn&& fn) {
   using std::integral_constant;
   return lattice_dispatch_sl(c, [&](auto sl, auto cb) -> hipError_t {
-    if (c.lpc_slotmajor) return fn(sl, cb, integral_constant<bool, false>{});
-    return fn(sl, cb, integral_constant<bool, true>{});
+    if (c.lpc_slotmajor) return fn(sl, cb, integral_constant<int, kDmSlotMajor>{});
+    if (c.lpc_split) return fn(sl, cb, integral_constant<int, kDmExt>{});
+    return fn(sl, cb, integral_constant<int, kDmContig>{});
   });
 }
 
@@ -2827,6 +3017,8 @@ hipError_t prepare_lpc_env(DevConsts& c) {
   c.lpc_lds_durbin = getenv("FDLP_LPC_LDS") != nullptr;
   c.lpc_cep_lds = getenv("FDLP_CEP_LDS") != nullptr;
   c.lpc_slotmajor = getenv("FDLP_LPC_SLOTMAJOR") != nullptr;
+  // the Durbin as its own kernel (durbin8_kernel) unless FDLP_LPC_FUSED=1 or the slot-major A/B form
+  c.lpc_split = !c.lpc_slotmajor && getenv("FDLP_LPC_FUSED") == nullptr && durbin8_fits(c.p);
   c.lpc_blocks = 0;
   int dev = 0, cus = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -2835,7 +3027,7 @@ hipError_t prepare_lpc_env(DevConsts& c) {
   int per_cu = 0;
   e = lattice_dispatch(c, [&](auto sl, auto cb, auto ct) -> hipError_t {
     constexpr int SL = decltype(sl)::value, CB = decltype(cb)::value;
-    constexpr bool CT = decltype(ct)::value;
+    constexpr int CT = decltype(ct)::value;
     const size_t lds = lattice_lds(c, CB, SL);
     if (lds > 65536) {
       const hipError_t a = hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL, CB, CT>,
@@ -2851,9 +3043,26 @@ hipError_t prepare_lpc_env(DevConsts& c) {
 }
 
 hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int items, double* env,
-                          double* a_out, double* gg_out, double* cep_out, hipStream_t s) {
+                          double* a_out, double* gg_out, double* cep_out, double* a_ws, double* gg_ws,
+                          hipStream_t s) {
   if (items <= 0) return hipSuccess;
   LpcEnvArgs A;
+  A.a_ext = nullptr;
+  A.gg_ext = nullptr;
+  if (c.lpc_blocks > 0 && c.lpc_split) {  // the Durbin first, into a_ws / gg_ws (the debug outputs if given)
+    double* ad = a_out ? a_out : a_ws;
+    double* gd = gg_out ? gg_out : gg_ws;
+    const hipError_t e = durbin8_dispatch(c.p, [&](auto sl8) -> hipError_t {
+      constexpr int SL8 = decltype(sl8)::value;
+      hipLaunchKernelGGL((durbin8_kernel<SL8>), dim3((items + 7) / 8), dim3(64), 0, s, r, c.nlags, c.p, items, ad, gd);
+      return hipGetLastError();
+    });
+    if (e != hipSuccess) return e;
+    A.a_ext = ad;
+    A.gg_ext = gd;
+    a_out = nullptr;  // already written
+    gg_out = nullptr;
+  }
   A.p = c.p; A.nlags = c.nlags; A.M = c.M; A.Me = c.Me; A.kk = c.kk; A.env_nfft = c.env_nfft;
   A.odd_zero = odd_zero; A.items = items; A.region = lpc_env_region(c.p, c.M); A.la_len = 0;
   A.r = r; A.weights = c.weights; A.env_cos = c.env_cos; A.env_win = c.env_win; A.env = env;
@@ -2862,7 +3071,7 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
     const int grid = std::min((items + 3) / 4, c.lpc_blocks);
     return lattice_dispatch(c, [&](auto sl, auto cb, auto ct) -> hipError_t {
       constexpr int SL = decltype(sl)::value, CB = decltype(cb)::value;
-      constexpr bool CT = decltype(ct)::value;
+      constexpr int CT = decltype(ct)::value;
       const size_t lds = lattice_lds(c, CB, SL);
       A.region = lattice_region(c, CB, SL);
       A.la_len = CB != 0 ? lattice_la_len(c, CB, SL) : 0;

@@ -896,7 +896,8 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
       HIP_TRY(fdlp::launch_autocorr(p->dc, p->ws.dct + f0 * N, nullptr, its, r, st));
     }
     HIP_TRY(mark(3));
-    HIP_TRY(fdlp::launch_lpc_env(p->dc, p->cfg.odd_mod_zero, r, its, env, a_dbg, gg_dbg, cep_dbg, st));
+    HIP_TRY(fdlp::launch_lpc_env(p->dc, p->cfg.odd_mod_zero, r, its, env, a_dbg, gg_dbg, cep_dbg,
+                                  p->ws.a + it0 * (p->p + 1), p->ws.gg + it0, st));
     HIP_TRY(mark(4));
     return FDLP_OK;
   };
