@@ -34,9 +34,6 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&d_cos, cosv.size() * 8));
   CK(hipMalloc(&d_win, win.size() * 8));
   CK(hipMalloc(&d_env, (size_t)items * kk * 8));
-  double *d_a, *d_gg;  // split Durbin workspace (durbin8_kernel)
-  CK(hipMalloc(&d_a, (size_t)items * (p + 1) * 8));
-  CK(hipMalloc(&d_gg, (size_t)items * 8));
   CK(hipMemcpy(d_r, r.data(), r.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_w, weights.data(), weights.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_cos, cosv.data(), cosv.size() * 8, hipMemcpyHostToDevice));
@@ -45,6 +42,9 @@ int main(int argc, char** argv) {
   c.p = p; c.nlags = nlags; c.M = M; c.Me = M < env_nfft ? M : env_nfft; c.kk = kk; c.env_nfft = env_nfft;
   c.weights = d_w; c.env_cos = d_cos; c.env_win = d_win;
   CK(fdlp::prepare_lpc_env(c));  // lattice kernel launch geometry (FDLP_LPC_SLOTMAJOR / FDLP_LPC_LDS read here)
+  double *d_a, *d_gg;  // split Durbin workspace (durbin8_kernel)
+  CK(hipMalloc(&d_a, (size_t)items * (c.lpc_astride > p + 1 ? c.lpc_astride : p + 1) * 8));
+  CK(hipMalloc(&d_gg, (size_t)items * 8));
   hipStream_t s;
   CK(hipStreamCreate(&s));
   for (int i = 0; i < 3; ++i) CK(fdlp::launch_lpc_env(c, 0, d_r, items, d_env, nullptr, nullptr, nullptr, d_a, d_gg, s));

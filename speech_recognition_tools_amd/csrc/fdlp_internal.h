@@ -89,6 +89,8 @@ struct DevConsts {
   int lpc_slotmajor = 0;   // FDLP_LPC_SLOTMAJOR at plan creation: the slot-major lattice Durbin
   int lpc_split = 0;       // the Durbin as durbin8_kernel (8 lanes per item), then the cepstrum/envelope
                            // kernel; off with FDLP_LPC_FUSED=1 (set by prepare_lpc_env)
+  int lpc_astride = 0;     // split Durbin: row stride of a_pad (the cepstrum kernel's a-area length,
+                           // zero past p), so a row is one contiguous LDS-DMA copy
   int dct_generic = 0;     // FDLP_DCT_GENERIC at plan creation: runtime-radix DCT passes for every N
 };
 
@@ -101,6 +103,7 @@ struct Workspace {
   double* dct;     // [F, N]
   double* r;       // [F*B, nlags]
   double* a;       // [F*B, p+1]
+  double* a_pad;   // [F*B, lpc_astride] (split Durbin only)
   double* gg;      // [F*B]
   double* cep;     // [F*B, M]
   double* env;     // [F*B, kk]
@@ -122,7 +125,8 @@ hipError_t launch_levinson(const DevConsts& c, const double* r, int items, doubl
                            double* gg, hipStream_t s);
 hipError_t launch_cepstrum(int p, int M, const double* a, const double* gg, int items,
                            double* cep, hipStream_t s);
-// a_ws / gg_ws: [items, p+1] / [items] workspace of the split Durbin (durbin8_kernel, c.lpc_split)
+// a_ws / gg_ws: [items, c.lpc_astride] / [items] workspace of the split Durbin (durbin8_kernel,
+// c.lpc_split); a_out / gg_out (debug, [items, p+1] / [items]) get copies
 hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int items, double* env,
                           double* a_out, double* gg_out, double* cep_out, double* a_ws, double* gg_ws,
                           hipStream_t s);

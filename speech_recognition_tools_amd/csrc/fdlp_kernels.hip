@@ -1822,8 +1822,9 @@ struct LpcEnvArgs {
   double* a_out;          // nullable [items, p+1]
   double* gg_out;         // nullable [items]
   double* cep_out;        // nullable [items, M]
-  const double* a_ext;    // DM = 2: a [items, p+1] and gg [items] from durbin8_kernel
+  const double* a_ext;    // DM = 2: a [items, a_stride] and gg [items] from durbin8_kernel
   const double* gg_ext;
+  int a_stride;
 };
 
 // Durbin recursion with a[] resident in LDS (la[0..p], zero beyond) and r in LDS (lr): lane l of
@@ -2141,7 +2142,7 @@ __device__ __forceinline__ void c8_relayout(const double (&A)[S], double (&An)[S
 template <int SL8, int S>
 __device__ __forceinline__ void c8_durbin(double (&A)[S], double (&B)[S], double (&R1)[S], double& part, double& E,
                                           const double* rl, double* sc, int p, int li, bool valid, double r0,
-                                          double* ao, double* go) {
+                                          double* ao, double* go, int astride) {
   const int k0 = S == 1 ? 1 : 8 * (S - 1);
   const int k1 = min(p + 1, 8 * S);
   const bool first = li == 0;
@@ -2165,7 +2166,7 @@ __device__ __forceinline__ void c8_durbin(double (&A)[S], double (&B)[S], double
     if (k1 <= p) {
       double An[S + 1], Bn[S + 1];
       c8_relayout<S>(A, An, Bn, sc, li);
-      c8_durbin<SL8, S + 1>(An, Bn, R1n, part, E, rl, sc, p, li, valid, r0, ao, go);
+      c8_durbin<SL8, S + 1>(An, Bn, R1n, part, E, rl, sc, p, li, valid, r0, ao, go, astride);
       return;
     }
   }
@@ -2177,21 +2178,21 @@ __device__ __forceinline__ void c8_durbin(double (&A)[S], double (&B)[S], double
     else q0 = fma(A[j], R1[j], q0);
   }
   const double gg = r0 + sum8(q0 + q1);
-  if (valid) {
+  if (valid) {  // the whole row: a_0 .. a_p, then zeros (A is exactly 0 past p) up to astride
 #pragma unroll
-    for (int j = 0; j < S; ++j)
-      if (li * S + j <= p) ao[li * S + j] = A[j];
+    for (int j = 0; j < S; ++j) ao[li * S + j] = A[j];
+    for (int m = 8 * S + li; m < astride; m += 8) ao[m] = 0.0;
     if (first) *go = gg;
   }
 }
 
-// one wave per 8 items (p + 1 <= 8 SL8); a / gg: [items, p + 1] / [items].  The 8 items' r rows are
+// one wave per 8 items (p + 1 <= 8 SL8 <= astride); a / gg: [items, astride] (zero past p) / [items].  The 8 items' r rows are
 // staged in LDS first (one coalesced pass), so each phase's R1 is an LDS read, not a global load
 // whose latency the short early phases cannot cover.  LDS per item: r_1 .. r_{8 SL8} and the relayout
 // image (8 zeros + 8 SL8); 8 items = 19.5 KB at SL8 = 19, two waves per SIMD.
 template <int SL8>
 __global__ __launch_bounds__(64, 2) void durbin8_kernel(const double* __restrict__ r, int nlags, int p, int items,
-                                                        double* __restrict__ a, double* __restrict__ gg) {
+                                                        double* __restrict__ a, double* __restrict__ gg, int astride) {
   constexpr int kR = 8 * SL8;
   constexpr int kItem = kR + 8 + 8 * SL8;
   __shared__ double lds[8 * kItem];
@@ -2217,8 +2218,8 @@ __global__ __launch_bounds__(64, 2) void durbin8_kernel(const double* __restrict
   c8_load_r1<1>(R11, rl, li);
   double part = li == 0 ? R11[0] : 0.0;  // order 1: b^(0) . R1 = r_1
   double E = r0;
-  c8_durbin<SL8, 1>(A1, B1, R11, part, E, rl, sc, p, li, valid, r0, a + (int64_t)(valid ? item : 0) * (p + 1),
-                    gg + (valid ? item : 0));
+  c8_durbin<SL8, 1>(A1, B1, R11, part, E, rl, sc, p, li, valid, r0, a + (int64_t)(valid ? item : 0) * astride,
+                    gg + (valid ? item : 0), astride);
 }
 
 // lpc_env with the lattice Durbin: persistent waves (grid-stride over groups of 4 items), r read
@@ -2254,6 +2255,24 @@ __global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(Lpc
     }
     if constexpr (DM != kDmExt) r0n = rr[0];
   };
+  // DM = 2 with a register cepstrum: the next group's a rows go global -> LDS by DMA (no registers)
+  // while this group's envelope runs (it reads only cs, not la)
+  auto dma_a = [&](int grp) {
+    if constexpr (DM == kDmExt && CB != 0) {
+#pragma unroll
+      for (int g2 = 0; g2 < 4; ++g2) {
+        const int it = min(grp * 4 + g2, A.items - 1);
+        const double* src = A.a_ext + (int64_t)it * A.a_stride;  // la_len doubles, 16-B aligned rows
+        double* dst = sh + g2 * A.region;
+        for (int c0 = 0; c0 < A.la_len; c0 += 128) {  // 64 lanes x 16 B = 128 doubles per copy
+          if (c0 + 2 * (int)threadIdx.x < A.la_len)
+            __builtin_amdgcn_global_load_lds((const void*)(src + c0 + 2 * threadIdx.x),
+                                             (__attribute__((address_space(3))) void*)(dst + c0), 16, 0, 0);
+        }
+      }
+    }
+  };
+  if (blockIdx.x < ngroups) dma_a(blockIdx.x);
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     load_r(grp);
     // Everything below is re-derived per group from opaque copies, so the compiler cannot hoist
@@ -2279,9 +2298,14 @@ __global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(Lpc
     // ---- phase 1: Levinson-Durbin (features.py:226-228) in registers -------------------------
     double gg;
     if constexpr (DM == kDmExt) {
-      const double* ai = A.a_ext + (int64_t)(valid ? item : 0) * (p + 1);
-      wave_lds_sync();  // the previous group's envelope reads of la are done
-      for (int q = l; q < NAL; q += 16) la[q] = (valid && q <= p) ? ai[q] : 0.0;
+      if constexpr (CB != 0) {
+        // la[0 .. la_len) = this group's a rows: LDS-DMA copies issued a group ahead (see below)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        const double* ai = A.a_ext + (int64_t)(valid ? item : 0) * A.a_stride;
+        wave_lds_sync();  // the previous group's envelope reads of la are done
+        for (int q = l; q < NAL; q += 16) la[q] = (valid && q <= p) ? ai[q] : 0.0;
+      }
       gg = valid ? A.gg_ext[item] : 1.0;
     } else if constexpr (CONTIG) {
       const double* rr = A.r + (int64_t)(valid ? item : 0) * A.nlags;
@@ -2432,6 +2456,7 @@ __global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(Lpc
       }
       wave_lds_sync();
     }
+    if (grp + (int)gridDim.x < ngroups) dma_a(grp + gridDim.x);  // la is free until the next group
     // ---- phase 3: weights + envelope (computeFDLPSpectrogram.py:194-205) ---------------------
     double* cw = CB != 0 ? cs : la;  // compact layout: weighted in place
     const double* mask = A.weights;
@@ -3003,7 +3028,7 @@ static int lattice_la_len(const DevConsts& c, int CB, int SL) {
   int la = std::max(c.p + 2, 16 * SL);
   if (CB > 0) la = std::max(la, 16 * CB);
   if (CB < 0) la = std::max(la, 16 * SL + 16);
-  return la;
+  return (la + 15) / 16 * 16;  // whole 128-B rows (the split Durbin's a rows are LDS-DMA copies)
 }
 static int lattice_region(const DevConsts& c, int CB, int SL) {
   const int need = CB != 0 ? lattice_la_len(c, CB, SL) + c.Me : (c.M > c.p + 1 ? c.M : c.p + 1) + 16 + c.M;
@@ -3019,6 +3044,7 @@ hipError_t prepare_lpc_env(DevConsts& c) {
   c.lpc_slotmajor = getenv("FDLP_LPC_SLOTMAJOR") != nullptr;
   // the Durbin as its own kernel (durbin8_kernel) unless FDLP_LPC_FUSED=1 or the slot-major A/B form
   c.lpc_split = !c.lpc_slotmajor && getenv("FDLP_LPC_FUSED") == nullptr && durbin8_fits(c.p);
+  c.lpc_astride = 0;
   c.lpc_blocks = 0;
   int dev = 0, cus = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -3029,6 +3055,7 @@ hipError_t prepare_lpc_env(DevConsts& c) {
     constexpr int SL = decltype(sl)::value, CB = decltype(cb)::value;
     constexpr int CT = decltype(ct)::value;
     const size_t lds = lattice_lds(c, CB, SL);
+    if (CT == kDmExt) c.lpc_astride = CB != 0 ? lattice_la_len(c, CB, SL) : (c.p + 1 + 15) / 16 * 16;
     if (lds > 65536) {
       const hipError_t a = hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL, CB, CT>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -3049,17 +3076,25 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
   LpcEnvArgs A;
   A.a_ext = nullptr;
   A.gg_ext = nullptr;
-  if (c.lpc_blocks > 0 && c.lpc_split) {  // the Durbin first, into a_ws / gg_ws (the debug outputs if given)
-    double* ad = a_out ? a_out : a_ws;
+  A.a_stride = 0;
+  if (c.lpc_blocks > 0 && c.lpc_split) {  // the Durbin first, into a_ws / gg_ws
+    if (!a_ws || !gg_ws) return hipErrorInvalidValue;
     double* gd = gg_out ? gg_out : gg_ws;
     const hipError_t e = durbin8_dispatch(c.p, [&](auto sl8) -> hipError_t {
       constexpr int SL8 = decltype(sl8)::value;
-      hipLaunchKernelGGL((durbin8_kernel<SL8>), dim3((items + 7) / 8), dim3(64), 0, s, r, c.nlags, c.p, items, ad, gd);
+      hipLaunchKernelGGL((durbin8_kernel<SL8>), dim3((items + 7) / 8), dim3(64), 0, s, r, c.nlags, c.p, items, a_ws, gd,
+                         c.lpc_astride);
       return hipGetLastError();
     });
     if (e != hipSuccess) return e;
-    A.a_ext = ad;
+    if (a_out) {  // debug: the [items, p+1] layout
+      const hipError_t e2 = hipMemcpy2DAsync(a_out, sizeof(double) * (c.p + 1), a_ws, sizeof(double) * c.lpc_astride,
+                                             sizeof(double) * (c.p + 1), items, hipMemcpyDeviceToDevice, s);
+      if (e2 != hipSuccess) return e2;
+    }
+    A.a_ext = a_ws;
     A.gg_ext = gd;
+    A.a_stride = c.lpc_astride;
     a_out = nullptr;  // already written
     gg_out = nullptr;
   }

@@ -401,7 +401,7 @@ int free_plan(fdlp_plan* p) {
     for (auto e : ev) (void)hipEventDestroy(e);
   void* devs[] = {p->d_fbank, p->d_hamming, p->d_weights, p->d_env_cos, p->d_env_win, p->d_tw1, p->d_post, p->d_rtw,
                   p->d_om1, p->d_om2, p->d_lo, p->d_hi, p->ws.z, p->ws.dct, p->ws.r, p->ws.a, p->ws.gg,
-                  p->ws.cep, p->ws.env, p->d_frames, p->d_utts, p->d_sk_e, p->r_up, p->d_sk_snap,
+                  p->ws.cep, p->ws.env, p->ws.a_pad, p->d_frames, p->d_utts, p->d_sk_e, p->r_up, p->d_sk_snap,
                   p->d_sk_reg, p->d_faxis, p->r_flat, p->d_fl_ev, p->r_flat_part, p->d_fl_band};
   for (void* d : devs)
     if (d) (void)hipFree(d);
@@ -697,6 +697,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
       hipMalloc((void**)&p->ws.r, sizeof(double) * items * p->nlags) != hipSuccess ||
       hipMalloc((void**)&p->ws.a, sizeof(double) * items * (p->p + 1)) != hipSuccess ||
       hipMalloc((void**)&p->ws.gg, sizeof(double) * items) != hipSuccess ||
+      (d.lpc_split && hipMalloc((void**)&p->ws.a_pad, sizeof(double) * items * d.lpc_astride) != hipSuccess) ||
       hipMalloc((void**)&p->ws.cep, sizeof(double) * items * M) != hipSuccess ||
       hipMalloc((void**)&p->ws.env, sizeof(double) * items * p->kk) != hipSuccess ||
       (p->sk_avail && hipMalloc((void**)&p->r_up, sizeof(double) * items * p->nlags) != hipSuccess) ||
@@ -897,7 +898,8 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     }
     HIP_TRY(mark(3));
     HIP_TRY(fdlp::launch_lpc_env(p->dc, p->cfg.odd_mod_zero, r, its, env, a_dbg, gg_dbg, cep_dbg,
-                                  p->ws.a + it0 * (p->p + 1), p->ws.gg + it0, st));
+                                  p->ws.a_pad ? p->ws.a_pad + it0 * p->dc.lpc_astride : nullptr, p->ws.gg + it0,
+                                  st));
     HIP_TRY(mark(4));
     return FDLP_OK;
   };

@@ -293,6 +293,63 @@ def modspec_fixtures():
     save("modspec_cochlear_rect", sig, opts, 0, run_reference_modspec(sig, opts))
 
 
+def run_reference_modspec_segments(recordings, segments, opts):
+    """computeModulationSpectrum_segments.getFeats (:24-116) with dict2Ark captured."""
+    sys.path.insert(0, os.path.join(REF, "src/featgen"))
+    import computeModulationSpectrum_segments as cmss  # noqa: E402
+    captured = {}
+    cmss.dict2Ark = lambda feat_dict, outfile, kaldi_cmd: captured.update(
+        {k: np.array(v) for k, v in feat_dict.items()})
+    with tempfile.TemporaryDirectory() as td:
+        scp = os.path.join(td, "wav.scp")
+        with open(scp, "w") as f:
+            for rec, x in recordings.items():
+                p = os.path.join(td, rec + ".wav")
+                wavfile.write(p, 16000, x)
+                f.write("%s %s\n" % (rec, p))
+        seg = os.path.join(td, "segments")
+        with open(seg, "w") as f:
+            for s_id, rec, t0, t1 in segments:
+                f.write("%s %s %s %s\n" % (s_id, rec, t0, t1))
+        ns = argparse.Namespace(scp=scp, segment=seg, outfile=os.path.join(td, "out"), add_reverb=None,
+                                set_unity_gain=opts.get("set_unity_gain", False),
+                                nmodulations=opts["nmodulations"], order=opts["order"],
+                                fduration=opts["fduration"], frate=opts["frate"], nfilters=opts["nfilters"],
+                                kaldi_cmd="true")
+        cmss.getFeats(ns)
+    return captured
+
+
+MODSPEC_SEG_DEFAULT = dict(nfilters=15, nmodulations=12, order=50, fduration=0.5, frate=100)
+
+
+def modspec_segments_fixtures():
+    """computeModulationSpectrum_segments.py: segments of two recordings (out of order, overlapping,
+    fractional times), default options and --set_unity_gain with other sizes."""
+    rec = OrderedDict()
+    rec["recA"] = speech_like(40000, 95)
+    rec["recB"] = speech_like(26000, 96)
+    segs = [("recA-000", "recA", "0.00", "0.75"), ("recA-001", "recA", "0.5", "1.9371"),
+            ("recB-000", "recB", "0.1", "1.6"), ("recA-002", "recA", "2.0", "2.5")]
+    meta_segs = [list(x) for x in segs]
+    feats = run_reference_modspec_segments(rec, segs, MODSPEC_SEG_DEFAULT)
+    save("modspec_segments", rec, MODSPEC_SEG_DEFAULT, 0, _seg_feats(feats, rec), extra=dict(segments=meta_segs),
+         more=_seg_more(feats))
+    opts = dict(MODSPEC_SEG_DEFAULT, nfilters=20, nmodulations=40, order=30, fduration=0.4, frate=50,
+                set_unity_gain=True)
+    feats = run_reference_modspec_segments(rec, segs, opts)
+    save("modspec_segments_unity", rec, opts, 0, _seg_feats(feats, rec), extra=dict(segments=meta_segs),
+         more=_seg_more(feats))
+
+
+def _seg_feats(feats, rec):  # save() stores out_<recording>; the per-segment outputs go in `more`
+    return {r: np.zeros((0,)) for r in rec}
+
+
+def _seg_more(feats):
+    return {"seg_" + k: v for k, v in feats.items()}
+
+
 def reverb_rir_fixture():
     """--add_reverb small_room (features.py:110-115) with a synthetic stereo RIR, clean and with noise."""
     rir = synthetic_rir(4000, 5)
@@ -320,6 +377,9 @@ def main():
         return
     if "--modspec-only" in sys.argv:
         modspec_fixtures()
+        return
+    if "--modspec-segments-only" in sys.argv:
+        modspec_segments_fixtures()
         return
     cli_options_fixture()
     if "--cli-only" in sys.argv:
@@ -387,6 +447,7 @@ def main():
     reverb_rir_fixture()
     mel_fixtures()
     modspec_fixtures()
+    modspec_segments_fixtures()
 
 
 if __name__ == "__main__":
