@@ -63,7 +63,7 @@ typedef struct fdlp_config {
                                 (0 = every non-zero tap; DESIGN.md "support")            */
   int32_t max_frames;        /* workspace capacity: analysis frames per fdlp_compute call  */
   /* ---- sibling feature: FDLP modulation spectrum (src/featgen/computeModulationSpectrum.py) ---- */
-  int32_t mode;              /* FDLP_MODE_SPECTROGRAM | FDLP_MODE_MODSPEC                          */
+  int32_t mode;              /* FDLP_MODE_SPECTROGRAM | FDLP_MODE_MODSPEC | FDLP_MODE_MODSPEC_COMPLEX */
   int32_t window;            /* analysis window: FDLP_WIN_HAMMING (spectrogram, :29) |
                                 FDLP_WIN_HANNING (modspec default, :30) | FDLP_WIN_RECT (--no_window) */
   int32_t coeff_0;           /* modspec --coeff_0 (1-based first kept coefficient); --coeff_n = coeff_num */
@@ -71,7 +71,9 @@ typedef struct fdlp_config {
   int32_t compensate_noise;  /* modspec --compensate_noise: x linspace(0, n/(2 fduration), coeff_n) (:82-88) */
   int32_t absolute_value;    /* modspec --absolute_value (:186-187)                                 */
 } fdlp_config;
-enum { FDLP_MODE_SPECTROGRAM = 0, FDLP_MODE_MODSPEC = 1 };
+enum { FDLP_MODE_SPECTROGRAM = 0, FDLP_MODE_MODSPEC = 1,
+       FDLP_MODE_MODSPEC_COMPLEX = 2 /* modspec --complex_modulation (computeModulationSpectrum.py:45-47,
+                                        :74-88, :153-180): ifft frames, complex LPC and cepstrum */ };
 enum { FDLP_WIN_HAMMING = 0, FDLP_WIN_HANNING = 1, FDLP_WIN_RECT = 2 };
 
 typedef struct fdlp_plan fdlp_plan;

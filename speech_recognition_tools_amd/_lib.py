@@ -30,6 +30,7 @@ FDLP_PRE_DIFF = 1
 FDLP_NUM_STAGES = 5
 FDLP_MODE_SPECTROGRAM = 0
 FDLP_MODE_MODSPEC = 1
+FDLP_MODE_MODSPEC_COMPLEX = 2
 FDLP_WIN_HAMMING = 0
 FDLP_WIN_HANNING = 1
 FDLP_WIN_RECT = 2

@@ -89,6 +89,8 @@ struct DevConsts {
   int lpc_slotmajor = 0;   // FDLP_LPC_SLOTMAJOR at plan creation: the slot-major lattice Durbin
   int lpc_split = 0;       // the Durbin as durbin8_kernel (8 lanes per item), then the cepstrum/envelope
                            // kernel; off with FDLP_LPC_FUSED=1 (set by prepare_lpc_env)
+  int natural = 0;         // complex modulation: frames in sample order, dft2 writes X = conj(DFT_N)/N
+                           // (scipy.fftpack.ifft of the real frame), bins [0, N/2), as double2 rows of N doubles
   int lpc_astride = 0;     // split Durbin: row stride of a_pad (the cepstrum kernel's a-area length,
                            // zero past p), so a row is one contiguous LDS-DMA copy
   int dct_generic = 0;     // FDLP_DCT_GENERIC at plan creation: runtime-radix DCT passes for every N
@@ -139,6 +141,13 @@ int band_fused_fits(int nlags, int p, int M, int kk);
 hipError_t launch_band_fused(const DevConsts& c, int odd_zero, const double* dct, int items, double* r_dbg,
                              double* env, hipStream_t s);
 constexpr int kDftMaxSub = 512;  // longest LDS-resident sub-DFT of the four-step DCT
+// Complex modulation spectrum (computeModulationSpectrum.py --complex_modulation): per (frame, band) the
+// complex circular autocorrelation of W_j X (lags 0..p+1), then Hermitian Levinson, complex gain and
+// cepstrum, and the feature slice (real/imag or abs, keep_even, 1/f compensation) into the output rows.
+hipError_t launch_cplx_modspec(const DevConsts& c, int L, const double* X, int nframes, double* ycplx,
+                               const FrameDesc* frames, const UttDesc* utts, int c0, int coeff_n, int feat_len,
+                               int step, int first, const double* faxis, int absval, float* out, double* out64,
+                               int decimals, hipStream_t s);
 hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc* frames,
                           const UttDesc* utts, int n_utt, int maxL, float* out,
                           double* out_f64, int decimals, hipStream_t s);

@@ -151,7 +151,8 @@ __device__ __forceinline__ double makhoul_sample(const DevConsts& c, const Frame
                                                  const int16_t* __restrict__ noise,
                                                  const double* __restrict__ dense_rows) {
   const int N = c.N;
-  const int m = (2 * n < N) ? 2 * n : 2 * N - 1 - 2 * n;  // Makhoul even/odd split
+  // Makhoul even/odd split; complex modulation: sample order (scipy.fftpack.ifft of the frame)
+  const int m = c.natural ? n : ((2 * n < N) ? 2 * n : 2 * N - 1 - 2 * n);
   if (dense_rows) return dense_rows[(int64_t)f * N + m];
   const int64_t t = reflect_idx((int64_t)fd.k * c.hop + m - c.ext, fd.T);
   double s;
@@ -297,6 +298,13 @@ __global__ __launch_bounds__(256) void dft2_dct_kernel(DevConsts c, DftPlan d2, 
       const double2 w1 = post[k], w2 = post[k + M];
       dct[(int64_t)f * N + k] = 2.0 * (w1.x * V1.x - w1.y * V1.y) / inv_scale_div;
       dct[(int64_t)f * N + k + M] = 2.0 * (w2.x * V2.x - w2.y * V2.y) / inv_scale_div;
+    } else if (c.natural) {
+      // complex modulation: ifft(frame)[k] = conj(DFT_k) / N (real frame), bins k < int(N/2)
+      // (computeModulationSpectrum.py:154-155); row f of N doubles holds them as double2
+      if (k < N / 2) {
+        const double inv = 1.0 / (double)N;
+        ((double2*)(dct + (int64_t)f * N))[k] = make_double2(V.x * inv, -V.y * inv);
+      }
     } else {
       const double2 w = post[k];
       const double y = 2.0 * (w.x * V.x - w.y * V.y);
@@ -3485,6 +3493,171 @@ __global__ __launch_bounds__(256) void modspec_out_kernel(const double* __restri
   const int64_t o = (utts[fd.utt].out_row + fd.k) * per + r;
   if (out64) out64[o] = v;
   if (out) out[o] = decimals >= 0 ? (float)(nearbyint(v * scale10) / scale10) : (float)v;
+}
+
+// -----------------------------------------------------------------------------------------
+// Complex modulation spectrum (computeModulationSpectrum.py --complex_modulation, :153-180).
+// cplx_autocorr_kernel: one wave per (frame, band) item, a lane per lag: with s = W_j X (the band's
+// complex spectrum, bins [0, L)), y[l] = sum_n s[(n + l) mod L] conj(s[n]) -- the circular
+// autocorrelation ifft(fft(s) conj(fft(s))) of computeLpcFast(keepreal=False) (features.py:223) as a
+// direct sum over the band's non-zero taps [lo, hi).
+// -----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void cplx_autocorr_kernel(DevConsts c, int L, const double* __restrict__ X,
+                                                           int items, double* __restrict__ y) {
+  const int item = blockIdx.x;
+  if (item >= items) return;
+  const int f = item / c.B, j = item % c.B;
+  const double2* Xr = (const double2*)(X + (int64_t)f * c.N);
+  const double* W = c.fbank + (int64_t)j * c.N;
+  const int lo = c.lo[j], hi = c.hi[j];
+  for (int l0 = 0; l0 < c.nlags; l0 += 64) {
+    const int l = l0 + (int)threadIdx.x;
+    const int lc = l < c.nlags ? l : 0;
+    double re = 0.0, im = 0.0;
+    for (int n = lo; n < hi; ++n) {
+      const double wn = W[n];
+      const double2 xn = Xr[n];
+      const double sr = wn * xn.x, si = wn * xn.y;  // s[n] = filt * cos_trans (features: band_dct)
+      int m = n + lc;
+      if (m >= L) m -= L;
+      const double wm = W[m];
+      const double2 xm = Xr[m];
+      const double tr = wm * xm.x, ti = wm * xm.y;
+      re = fma(tr, sr, fma(ti, si, re));     // Re s[m] conj(s[n])
+      im = fma(ti, sr, fma(-tr, si, im));    // Im
+    }
+    if (l < c.nlags) {
+      y[((int64_t)item * c.nlags + l) * 2] = re;
+      y[((int64_t)item * c.nlags + l) * 2 + 1] = im;
+    }
+  }
+}
+
+__device__ __forceinline__ double2 wave_sum2(double2 v) { return make_double2(wave_sum(v.x), wave_sum(v.y)); }
+__device__ __forceinline__ double2 cmul2(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// numpy's principal complex sqrt (npy_csqrt) and log
+__device__ __forceinline__ double2 csqrt_np(double2 z) {
+  if (z.x == 0.0 && z.y == 0.0) return make_double2(0.0, z.y);
+  const double t = sqrt((fabs(z.x) + hypot(z.x, z.y)) * 0.5);
+  if (z.x >= 0.0) return make_double2(t, z.y / (2.0 * t));
+  return make_double2(fabs(z.y) / (2.0 * t), copysign(t, z.y));
+}
+__device__ __forceinline__ double2 clog_np(double2 z) { return make_double2(log(hypot(z.x, z.y)), atan2(z.y, z.x)); }
+
+// cplx_lpc_out_kernel: one wave per item.  Levinson-Durbin on the Hermitian Toeplitz system of
+// solve_toeplitz(y[0:p], -y[1:p+1]) (features.py:226; a_i += kappa conj(a_{k-i})), the complex gain
+// gg = y[0] + sum a_i y[i+1] (:228), the complex cepstrum computeModSpecFromLpc (:233-246, c_0 =
+// log(sqrt(gg)) on numpy's principal branches), then [* faxis], abs or (real, imag) of the slice
+// [c0, coeff_n), keep_even (step 2 from `first`) into the item's output columns (:174-201).
+__global__ __launch_bounds__(64) void cplx_lpc_out_kernel(const double* __restrict__ ycplx, int items, int B, int p,
+                                                          int nlags, int coeff_n, const FrameDesc* __restrict__ frames,
+                                                          const UttDesc* __restrict__ utts, int c0, int feat_len,
+                                                          int step, int first, const double* __restrict__ faxis,
+                                                          int absval, float* __restrict__ out, double* __restrict__ out64,
+                                                          int decimals, double scale10) {
+  extern __shared__ double2 csh[];
+  const int item = blockIdx.x;
+  if (item >= items) return;
+  const int lane = threadIdx.x;
+  const int NA = (p + 1 > coeff_n + 1 ? p + 1 : coeff_n + 1);
+  double2* ys = csh;             // nlags
+  double2* a = ys + nlags;       // NA: a_0 .. a_p, zeros beyond (alpha = -a past the order is 0)
+  double2* cep = a + NA;         // coeff_n
+  const double2* yi = (const double2*)ycplx + (int64_t)item * nlags;
+  for (int l = lane; l < nlags; l += 64) ys[l] = yi[l];
+  for (int i = lane; i < NA; i += 64) a[i] = make_double2(i == 0 ? 1.0 : 0.0, 0.0);
+  __syncthreads();
+  double E = ys[0].x;
+  for (int k = 1; k <= p; ++k) {
+    double2 part = make_double2(0.0, 0.0);
+    for (int i = 1 + lane; i < k; i += 64) {
+      const double2 t = cmul2(a[i], ys[k - i]);
+      part.x += t.x;
+      part.y += t.y;
+    }
+    const double2 acc = wave_sum2(part);
+    const double2 yk = ys[k];
+    const double2 kap = make_double2(-(yk.x + acc.x) / E, -(yk.y + acc.y) / E);
+    double2 nv[4];
+    int cnt = 0;
+    for (int i = 1 + lane; i < k; i += 64, ++cnt) {
+      const double2 am = a[k - i];
+      const double2 t = cmul2(kap, make_double2(am.x, -am.y));
+      nv[cnt & 3] = make_double2(a[i].x + t.x, a[i].y + t.y);
+    }
+    __syncthreads();
+    cnt = 0;
+    for (int i = 1 + lane; i < k; i += 64, ++cnt) a[i] = nv[cnt & 3];
+    if (lane == 0) a[k] = kap;
+    __syncthreads();
+    E = E * (1.0 - (kap.x * kap.x + kap.y * kap.y));
+  }
+  // gg = y[0] + sum_{i=0}^{p} a_i y[i+1]
+  double2 part = make_double2(0.0, 0.0);
+  for (int i = lane; i <= p; i += 64) {
+    const double2 t = cmul2(a[i], ys[i + 1]);
+    part.x += t.x;
+    part.y += t.y;
+  }
+  const double2 sg = wave_sum2(part);
+  const double2 gg = make_double2(ys[0].x + sg.x, ys[0].y + sg.y);
+  // cepstrum: alpha_i = -a_i
+  if (lane == 0) {
+    cep[0] = clog_np(csqrt_np(gg));
+    if (coeff_n > 1) cep[1] = make_double2(-a[1].x, -a[1].y);
+  }
+  __syncthreads();
+  for (int n = 2; n < coeff_n; ++n) {
+    double2 q = make_double2(0.0, 0.0);
+    for (int k = 1 + lane; k < n; k += 64) {
+      const double w = (double)k / (double)n;                 // aa = arange(1, n) / n
+      const double2 al = make_double2(-a[n - k].x, -a[n - k].y);  // bb = flipud(alpha[1:n])
+      const double2 t = cmul2(make_double2(w * al.x, w * al.y), cep[k]);
+      q.x += t.x;
+      q.y += t.y;
+    }
+    const double2 sq = wave_sum2(q);
+    if (lane == 0) cep[n] = make_double2(sq.x - a[n].x, sq.y - a[n].y);  // + alpha_n
+    __syncthreads();
+  }
+  const int sel = coeff_n - c0;
+  const int f = item / B, j = item % B;
+  const FrameDesc fd = frames[f];
+  const int64_t row = (utts[fd.utt].out_row + fd.k) * (int64_t)B * feat_len + (int64_t)j * feat_len;
+  for (int i = lane; i < feat_len; i += 64) {
+    const int qq = first + step * i;  // temp2 index
+    double v;
+    if (absval) {
+      double2 z = cep[c0 + qq];
+      if (faxis) z = make_double2(z.x * faxis[c0 + qq], z.y * faxis[c0 + qq]);
+      v = hypot(z.x, z.y);
+    } else {
+      const int nn = qq < sel ? qq : qq - sel;
+      double2 z = cep[c0 + nn];
+      if (faxis) z = make_double2(z.x * faxis[c0 + nn], z.y * faxis[c0 + nn]);
+      v = qq < sel ? z.x : z.y;
+    }
+    if (out64) out64[row + i] = v;
+    if (out) out[row + i] = decimals >= 0 ? (float)(nearbyint(v * scale10) / scale10) : (float)v;
+  }
+}
+
+hipError_t launch_cplx_modspec(const DevConsts& c, int L, const double* X, int nframes, double* ycplx,
+                               const FrameDesc* frames, const UttDesc* utts, int c0, int coeff_n, int feat_len,
+                               int step, int first, const double* faxis, int absval, float* out, double* out64,
+                               int decimals, hipStream_t s) {
+  const int items = nframes * c.B;
+  if (items <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cplx_autocorr_kernel, dim3(items), dim3(64), 0, s, c, L, X, items, ycplx);
+  double scale10 = 1.0;
+  for (int i = 0; i < decimals; ++i) scale10 *= 10.0;
+  const int NA = std::max(c.p + 1, coeff_n + 1);
+  const size_t lds = sizeof(double2) * ((size_t)c.nlags + NA + coeff_n);
+  hipLaunchKernelGGL(cplx_lpc_out_kernel, dim3(items), dim3(64), lds, s, ycplx, items, c.B, c.p, c.nlags, coeff_n,
+                     frames, utts, c0, feat_len, step, first, faxis, absval, out, out64, decimals, scale10);
+  return hipGetLastError();
 }
 
 hipError_t launch_modspec_out(const double* cep, const FrameDesc* frames, const UttDesc* utts, int nframes, int B,

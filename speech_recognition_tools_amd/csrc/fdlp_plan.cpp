@@ -365,6 +365,8 @@ struct fdlp_plan {
   int2* d_sk_reg = nullptr;
   // modulation-spectrum mode (computeModulationSpectrum.py)
   bool modspec = false;
+  bool cplx = false;      // modspec --complex_modulation (FDLP_MODE_MODSPEC_COMPLEX)
+  int L = 0;              // cplx: int(fduration srate / 2) ifft bins (computeModulationSpectrum.py:155)
   int feat_len = 0, out_dim = 0;
   double* d_faxis = nullptr;  // [coeff_n] compensate_noise multipliers, null otherwise
   std::vector<std::vector<hipEvent_t>> prof_pending;
@@ -497,12 +499,15 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   p->N = (int)((double)c.srate * c.fduration);                       // features.py:134
   const double lfr = 1.0 / (ov * c.fduration);                       // :174
   p->hop = (int)((double)c.srate / lfr);                             // features.py:135
-  p->modspec = c.mode == FDLP_MODE_MODSPEC;
+  p->modspec = c.mode == FDLP_MODE_MODSPEC || c.mode == FDLP_MODE_MODSPEC_COMPLEX;
+  p->cplx = c.mode == FDLP_MODE_MODSPEC_COMPLEX;
   if (c.mode != FDLP_MODE_SPECTROGRAM && !p->modspec) PLAN_FAIL(FDLP_E_INVALID, "unknown plan mode");
+  p->L = (int)(c.fduration * (double)c.srate / 2.0);  // cos_trans[:, :int(fduration * srate / 2)] (:155)
   if (p->modspec) p->hop = (int)((double)c.srate / (double)c.frate);  // getFrames(.., frate, ..) (:150-151)
   if (p->N % 2 == 0) { p->sp_b = p->N / 2 - 1; p->sp_f = p->N / 2; p->ext = p->N / 2 - 1; }
   else { p->sp_b = p->sp_f = p->ext = (p->N - 1) / 2; }
   p->nfft = (int)(2.0 * c.fduration * (double)c.srate);              // :53, :59
+  if (p->cplx) p->nfft = (int)(c.fduration * (double)c.srate);        // dur (computeModulationSpectrum.py:45-46)
   p->env_nfft = 2 * (int)(c.fduration * (double)c.frate);            // :201
   p->kk = (int)nearbyint(c.fduration * (double)c.frate);             // :203 (np.round: half-even)
   p->kkb2 = (int)nearbyint(c.fduration * (double)c.frate / 2.0);     // :204
@@ -516,8 +521,12 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
     if (c.coeff_0 < 1 || c.coeff_0 > c.coeff_num) PLAN_FAIL(FDLP_E_INVALID, "modspec needs 1 <= coeff_0 <= coeff_n");
     if (c.gamma_enabled || c.lifter || c.odd_mod_zero) PLAN_FAIL(FDLP_E_INVALID, "modspec takes no gamma/lifter/odd options");
     const int sel = c.coeff_num - c.coeff_0 + 1;                     // coeff_num (:64)
-    p->feat_len = c.keep_even ? ((c.coeff_0 % 2 == 0) ? sel / 2 : (sel + 1) / 2) : sel;  // :66-80
+    p->feat_len = c.keep_even ? ((c.coeff_0 % 2 == 0) ? sel / 2 : (sel + 1) / 2)  // :66-80
+                  : (p->cplx && !c.absolute_value ? 2 * sel : sel);
     if (p->feat_len < 1) PLAN_FAIL(FDLP_E_INVALID, "modspec selects no coefficient");
+    if (p->cplx && c.keep_even && !c.absolute_value)  // temp2 has 2 sel values, feat_len ~ sel / 2 (:191-197)
+      PLAN_FAIL(FDLP_E_INVALID, "complex_modulation with keep_even needs absolute_value (reference broadcast error)");
+    if (p->cplx && c.coeff_num > 1024) PLAN_FAIL(FDLP_E_INVALID, "complex_modulation: coeff_n too large (max 1024)");
   }
   p->Me = std::min(p->M, p->env_nfft);
   p->out_dim = p->modspec ? c.nfilters * p->feat_len : c.nfilters;
@@ -529,7 +538,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   if ((p->p + 1 + 15) / 16 > 15) PLAN_FAIL(FDLP_E_INVALID, "order too large for the Levinson kernel");
   if (p->kk > 256) PLAN_FAIL(FDLP_E_INVALID, "fduration*frate too large (envelope > 256 samples)");
   if (p->M > 4096) PLAN_FAIL(FDLP_E_INVALID, "coeff_num too large (max 4096)");
-  p->real_fft = p->N % 2 == 0 && split_four_step(p->N / 2, &p->d1, &p->d2);
+  p->real_fft = !p->cplx && p->N % 2 == 0 && split_four_step(p->N / 2, &p->d1, &p->d2);
   p->nfft_c = p->real_fft ? p->N / 2 : p->N;  // complex FFT length of the DCT
   if (!p->real_fft && !split_four_step(p->nfft_c, &p->d1, &p->d2))
     PLAN_FAIL(FDLP_E_INVALID, "frame length int(srate*fduration) has no supported 2/3/5/7 four-step split");
@@ -542,20 +551,22 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   } else {
     PLAN_FAIL(FDLP_E_INVALID, "Invalid type of filter bank, use mel or cochlear with proper configuration");
   }
-  if (p->ncol - 1 != p->N)  // filt (ncol-1 taps) * cos_trans[i, :] (N) must broadcast (:190-191)
+  const int width = p->cplx ? p->L : p->N;  // taps of filt = fbank[j, :-1]
+  if (p->ncol - 1 != width)  // filt (ncol-1 taps) * cos_trans[i, :] (N, or L ifft bins) must broadcast (:190-191)
     PLAN_FAIL(FDLP_E_INVALID, "filterbank width nfft/2 does not match the frame length (reference broadcast error)");
-  std::vector<double> dense((size_t)p->B * p->N);
+  if (p->cplx && p->nlags > p->L) PLAN_FAIL(FDLP_E_INVALID, "complex_modulation: order + 2 exceeds the ifft bins");
+  std::vector<double> dense((size_t)p->B * p->N);  // rows of N (cplx: the L taps, zeros beyond)
   p->lo.assign(p->B, 0);
   p->hi.assign(p->B, 0);
   for (int j = 0; j < p->B; ++j) {
     const double* row = &p->fbank_host[(size_t)j * p->ncol];
     double peak = 0.0;
-    for (int m = 0; m < p->N; ++m) peak = std::max(peak, std::fabs(row[m]));
-    const double thr = c.support_eps > 0 ? c.support_eps * peak : 0.0;
+    for (int m = 0; m < width; ++m) peak = std::max(peak, std::fabs(row[m]));
+    const double thr = c.support_eps > 0 && !p->cplx ? c.support_eps * peak : 0.0;
     int lo = p->N, hi = 0;
-    for (int m = 0; m < p->N; ++m) {
+    for (int m = 0; m < width; ++m) {
       dense[(size_t)j * p->N + m] = row[m];
-      const bool keep = c.support_eps > 0 ? std::fabs(row[m]) >= thr : row[m] != 0.0;
+      const bool keep = thr > 0 ? std::fabs(row[m]) >= thr : row[m] != 0.0;
       if (keep) { lo = std::min(lo, m); hi = m + 1; }
     }
     if (hi <= lo) { lo = 0; hi = 0; }
@@ -563,7 +574,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
     p->hi[j] = hi;
   }
 
-  p->sk_avail = skirt_tables(c, p->B, p->N, p->nfft, &p->sk);
+  p->sk_avail = !p->cplx && skirt_tables(c, p->B, p->N, p->nfft, &p->sk);
   p->vs_avail = p->sk_avail && p->sk.fl_C > 0 && fdlp::vsweep_chains(p->sk.fl_C) > 0 &&
                 fdlp::vsweep_lanes_lags(p->nlags) > 0;
   p->ac_path = !p->sk_avail || getenv("FDLP_AUTOCORR_DIRECT") ? FDLP_AC_DIRECT
@@ -649,7 +660,8 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   PLAN_TRY(upload(&p->d_hi, p->hi.data(), p->hi.size()));
   PLAN_TRY(upload(&p->d_hamming, ham.data(), ham.size()));
   if (p->modspec && c.compensate_noise) {  // faxis = linspace(0, coeff_num / (2 fduration), coeff_n) (:86-88)
-    const double fmax = (double)(c.coeff_num - c.coeff_0 + 1) / (2.0 * c.fduration);
+    // complex: linspace(0, coeff_num / fduration, coeff_n) (:83-85)
+    const double fmax = (double)(c.coeff_num - c.coeff_0 + 1) / ((p->cplx ? 1.0 : 2.0) * c.fduration);
     const std::vector<double> fax = linspace(0.0, fmax, c.coeff_num);
     PLAN_TRY(upload(&p->d_faxis, fax.data(), fax.size()));
   }
@@ -667,7 +679,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   d.kk = p->kk; d.env_nfft = p->env_nfft;
   d.fbank = p->d_fbank; d.lo = p->d_lo; d.hi = p->d_hi; d.hamming = p->d_hamming; d.weights = p->d_weights;
   d.env_cos = p->d_env_cos; d.env_win = p->d_env_win; d.tw1 = p->d_tw1; d.post = p->d_post;
-  d.rtw = p->d_rtw; d.real_fft = p->real_fft ? 1 : 0;
+  d.rtw = p->d_rtw; d.real_fft = p->real_fft ? 1 : 0; d.natural = p->cplx ? 1 : 0;
   if (p->sk_avail) {
     PLAN_TRY(upload(&p->d_sk_e, p->sk.e.data(), p->sk.e.size()));
     PLAN_TRY(upload(&p->d_sk_snap, p->sk.snap.data(), p->sk.snap.size()));
@@ -694,7 +706,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   p->max_frames = c.max_frames;
   if (hipMalloc((void**)&p->ws.z, sizeof(double2) * F * p->nfft_c) != hipSuccess ||
       hipMalloc((void**)&p->ws.dct, sizeof(double) * F * N) != hipSuccess ||
-      hipMalloc((void**)&p->ws.r, sizeof(double) * items * p->nlags) != hipSuccess ||
+      hipMalloc((void**)&p->ws.r, sizeof(double) * items * p->nlags * (p->cplx ? 2 : 1)) != hipSuccess ||
       hipMalloc((void**)&p->ws.a, sizeof(double) * items * (p->p + 1)) != hipSuccess ||
       hipMalloc((void**)&p->ws.gg, sizeof(double) * items) != hipSuccess ||
       (d.lpc_split && hipMalloc((void**)&p->ws.a_pad, sizeof(double) * items * d.lpc_astride) != hipSuccess) ||
@@ -881,6 +893,16 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     HIP_TRY(mark(1));
     HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z + f0 * p->nfft_c, n, p->ws.dct + f0 * N, p->d_om2, st));
     HIP_TRY(mark(2));
+    if (p->cplx) {  // complex modulation: autocorrelation, LPC, cepstrum and the output columns
+      const fdlp_config& c = p->cfg;
+      HIP_TRY(fdlp::launch_cplx_modspec(p->dc, p->L, p->ws.dct + f0 * N, n, p->ws.r + it0 * nl * 2, p->d_frames + f0,
+                                        p->d_utts, c.coeff_0 - 1, p->M, p->feat_len, c.keep_even ? 2 : 1,
+                                        c.keep_even && c.coeff_0 % 2 == 0 ? 1 : 0, p->d_faxis, c.absolute_value,
+                                        b->out_dev, b->out_f64_dev, b->ark_decimals, st));
+      HIP_TRY(mark(3));
+      HIP_TRY(mark(4));
+      return FDLP_OK;
+    }
     if (p->ac_path == FDLP_AC_STRUCTURED || p->ac_path == FDLP_AC_STRUCTURED_MFMA) {
       double* rflat = p->ac_path == FDLP_AC_STRUCTURED ? p->r_flat + it0 * nl : nullptr;
       double* rpart = p->ac_path == FDLP_AC_STRUCTURED && p->r_flat_part
@@ -918,13 +940,13 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     HIP_TRY(hipStreamWaitEvent(s, p->ev_join, 0));
   }
   if (p->profiling) HIP_TRY(hipEventRecord(ev[ev.size() - 2], s));
-  if (p->modspec) {  // mod_spec[coeff_0-1 : coeff_n] per band (computeModulationSpectrum.py:182-201)
+  if (p->modspec && !p->cplx) {  // mod_spec[coeff_0-1 : coeff_n] per band (computeModulationSpectrum.py:182-201)
     const fdlp_config& c = p->cfg;
     const int keep_odd_slot = c.keep_even && c.coeff_0 % 2 == 0 ? 1 : 0;  // temp2[1::2] vs temp2[0::2]
     HIP_TRY(fdlp::launch_modspec_out(p->ws.cep, p->d_frames, p->d_utts, (int)nf, p->B, p->M, c.coeff_0 - 1,
                                      p->feat_len, c.keep_even ? 2 : 1, keep_odd_slot, p->d_faxis,
                                      c.absolute_value, b->out_dev, b->out_f64_dev, b->ark_decimals, s));
-  } else {
+  } else if (!p->modspec) {  // (complex modulation: the rows were written by launch_cplx_modspec)
     HIP_TRY(fdlp::launch_ola_log(p->dc, p->ws.env, p->d_frames, p->d_utts, b->n_utt, maxL, b->out_dev,
                                  b->out_f64_dev, b->ark_decimals, s));
   }

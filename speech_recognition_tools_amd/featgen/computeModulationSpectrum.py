@@ -7,8 +7,10 @@ the frame/DCT/autocorrelation/lattice-LPC kernels of compute-fdlp-feats and ends
 
 Same positional arguments, options, defaults and outputs (<outfile>.ark/.scp, '%.3f' rounding of dict2Ark,
 features.py:63-69); the ark is written natively, --kaldi_cmd is accepted and ignored.  --complex_modulation
-(the ifft/complex-LPC branch, :45-47/:152-180) is not implemented and fails up front.  --set_unity_gain is
-accepted and, as in the reference, has no effect.  Additions: --device, --batch_frames, --io_workers,
+(the ifft/complex-LPC branch, :45-47/:74-88/:152-180) runs as the plan's FDLP_MODE_MODSPEC_COMPLEX (ifft
+frames, complex autocorrelation + Hermitian Levinson + complex cepstrum kernels); with --keep_even it needs
+--absolute_value (otherwise the reference fails with a broadcast error, and so does this).  --set_unity_gain
+is accepted and, as in the reference, has no effect.  Additions: --device, --batch_frames, --io_workers,
 --ark_precision.
 """
 import argparse
@@ -55,9 +57,8 @@ def get_args(argv=None):
 def feature_config(args, srate=16000):
     """getFeats :30-92 as a plan configuration."""
     from speech_recognition_tools_amd.plan import FeatureConfig
-    if args.complex_modulation:
-        raise NotImplementedError("--complex_modulation (ifft + complex LPC) is not supported on the device path")
-    return FeatureConfig(mode="modspec", window="rect" if args.no_window else "hanning",
+    return FeatureConfig(mode="modspec_complex" if args.complex_modulation else "modspec",
+                         window="rect" if args.no_window else "hanning",
                          nfilters=args.nfilters, coeff_num=args.coeff_n, coeff_0=args.coeff_0, order=args.order,
                          fduration=args.fduration, frate=args.frate, fbank_type=args.fbank_type,
                          keep_even=bool(args.keep_even), compensate_noise=bool(args.compensate_noise),

@@ -33,7 +33,8 @@ class FeatureConfig:
     lifter: Optional[Sequence[float]] = None
     srate: int = 16000
     support_eps: float = DEFAULT_SUPPORT_EPS
-    # modulation spectrum (computeModulationSpectrum.py): mode "modspec", coeff_num = --coeff_n
+    # modulation spectrum (computeModulationSpectrum.py): mode "modspec" ("modspec_complex" with
+    # --complex_modulation), coeff_num = --coeff_n
     mode: str = "spectrogram"
     window: str = "hamming"           # "hamming" (:29) | "hanning" (modspec :30) | "rect" (--no_window)
     coeff_0: int = 1
@@ -72,7 +73,8 @@ class FeatureConfig:
             c.lifter, c.lifter_len = ptr(keep, ctypes.c_double), keep.size
         c.support_eps = float(self.support_eps)
         c.max_frames = int(max_frames)
-        c.mode = {"spectrogram": _lib.FDLP_MODE_SPECTROGRAM, "modspec": _lib.FDLP_MODE_MODSPEC}[self.mode]
+        c.mode = {"spectrogram": _lib.FDLP_MODE_SPECTROGRAM, "modspec": _lib.FDLP_MODE_MODSPEC,
+                  "modspec_complex": _lib.FDLP_MODE_MODSPEC_COMPLEX}[self.mode]
         c.window = {"hamming": _lib.FDLP_WIN_HAMMING, "hanning": _lib.FDLP_WIN_HANNING,
                     "rect": _lib.FDLP_WIN_RECT}[self.window]
         c.coeff_0, c.keep_even = int(self.coeff_0), int(bool(self.keep_even))

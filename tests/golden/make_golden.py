@@ -267,7 +267,8 @@ def run_reference_modspec(signals, opts):
         ns = argparse.Namespace(scp=scp, outfile=os.path.join(td, "out"), scp_type="wav", add_reverb="clean",
                                 coeff_0=opts["coeff_0"], coeff_n=opts["coeff_n"], order=opts["order"],
                                 fduration=opts["fduration"], frate=opts["frate"], nfilters=opts["nfilters"],
-                                kaldi_cmd="true", fbank_type=opts["fbank_type"], complex_modulation=False,
+                                kaldi_cmd="true", fbank_type=opts["fbank_type"],
+                                complex_modulation=opts.get("complex_modulation", False),
                                 keep_even=opts.get("keep_even", False),
                                 compensate_noise=opts.get("compensate_noise", False),
                                 no_window=opts.get("no_window", False),
@@ -291,6 +292,24 @@ def modspec_fixtures():
     opts = dict(MODSPEC_DEFAULT, nfilters=20, coeff_0=2, coeff_n=24, order=40, fduration=0.4, frate=50,
                 fbank_type="cochlear,1,1,1,2.5,1", keep_even=True, no_window=True)
     save("modspec_cochlear_rect", sig, opts, 0, run_reference_modspec(sig, opts))
+    modspec_complex_fixtures()
+
+
+def modspec_complex_fixtures():
+    """--complex_modulation (computeModulationSpectrum.py:45-47, :74-88, :153-180): real+imag, and
+    abs + compensate_noise + keep_even; a cochlear filterbank with abs and a rectangular window."""
+    sig = OrderedDict()
+    sig["q1"] = speech_like(9000, 91)
+    sig["q2"] = speech_like(4100, 92)
+    sig["qwhite"] = white(3000, 93)
+    opts = dict(MODSPEC_DEFAULT, complex_modulation=True)
+    save("modspec_complex", sig, opts, 0, run_reference_modspec(sig, opts))
+    opts = dict(MODSPEC_DEFAULT, complex_modulation=True, keep_even=True, compensate_noise=True,
+                absolute_value=True)
+    save("modspec_complex_even_comp_abs", sig, opts, 0, run_reference_modspec(sig, opts))
+    opts = dict(MODSPEC_DEFAULT, nfilters=20, coeff_0=2, coeff_n=24, order=40, fduration=0.4, frate=50,
+                fbank_type="cochlear,1,1,1,2.5,1", complex_modulation=True, absolute_value=True, no_window=True)
+    save("modspec_complex_cochlear_rect", sig, opts, 0, run_reference_modspec(sig, opts))
 
 
 def run_reference_modspec_segments(recordings, segments, opts):
@@ -377,6 +396,9 @@ def main():
         return
     if "--modspec-only" in sys.argv:
         modspec_fixtures()
+        return
+    if "--modspec-complex-only" in sys.argv:
+        modspec_complex_fixtures()
         return
     if "--modspec-segments-only" in sys.argv:
         modspec_segments_fixtures()

@@ -14,6 +14,7 @@ from oracle import mel_oracle as MO
 from oracle import modspec_oracle as MS
 
 MODSPEC_SETS = ["modspec_default", "modspec_even_comp_abs", "modspec_cochlear_rect"]
+COMPLEX_SETS = ["modspec_complex", "modspec_complex_even_comp_abs", "modspec_complex_cochlear_rect"]
 TOL = 1e-7
 
 
@@ -26,9 +27,37 @@ def test_modspec_oracle_matches_reference(name):
         np.testing.assert_allclose(got, ref[u], rtol=1e-9, atol=1e-9)
 
 
+def _opts(o):
+    o = dict(o)
+    o.pop("complex_modulation", None)
+    return o
+
+
+@pytest.mark.parametrize("name", COMPLEX_SETS)
+def test_modspec_complex_oracle_matches_reference(name):
+    meta, sig, ref, _ = load_golden(name)
+    for u in meta["utts"]:
+        got = MS.modspec_complex_features(sig[u].astype(np.float64), **_opts(meta["opts"]))
+        assert got.shape == ref[u].shape, u
+        np.testing.assert_allclose(got, ref[u], rtol=1e-9, atol=1e-9)
+
+
+def test_modspec_complex_geometry_and_validation():
+    from speech_recognition_tools_amd._lib import FdlpError
+    from speech_recognition_tools_amd.plan import FdlpPlan, FeatureConfig
+    for name in COMPLEX_SETS:
+        meta, _, ref, _ = load_golden(name)
+        plan = FdlpPlan(_cfg(meta["opts"]), device=-1, max_frames=16)
+        assert plan.out_dim == ref[meta["utts"][0]].shape[1], name
+    with pytest.raises(FdlpError):  # keep_even without abs: the reference's broadcast error
+        FdlpPlan(FeatureConfig(mode="modspec_complex", nfilters=15, coeff_num=30, coeff_0=5, order=50,
+                               keep_even=True), device=-1)
+
+
 def _cfg(o):
     from speech_recognition_tools_amd.plan import FeatureConfig
-    return FeatureConfig(mode="modspec", window="rect" if o.get("no_window") else "hanning",
+    return FeatureConfig(mode="modspec_complex" if o.get("complex_modulation") else "modspec",
+                         window="rect" if o.get("no_window") else "hanning",
                          nfilters=o["nfilters"], coeff_num=o["coeff_n"], coeff_0=o["coeff_0"], order=o["order"],
                          fduration=o["fduration"], frate=o["frate"], fbank_type=o["fbank_type"],
                          keep_even=bool(o.get("keep_even")), compensate_noise=bool(o.get("compensate_noise")),
@@ -64,8 +93,7 @@ def test_modspec_cli_args():
         (15, 5, 30, 50, 0.5, 100, "mel,1")
     c = feature_config(get_args(["s.scp", "out", "--no_window", "--keep_even", "--coeff_0=2"]))
     assert c.mode == "modspec" and c.window == "rect" and c.keep_even and c.coeff_0 == 2
-    with pytest.raises(NotImplementedError):
-        feature_config(get_args(["s.scp", "out", "--complex_modulation"]))
+    assert feature_config(get_args(["s.scp", "out", "--complex_modulation"])).mode == "modspec_complex"
 
 
 def _modspec_gpu(cfg, sig, utts, rir=None, max_frames=4096):
@@ -87,6 +115,19 @@ def _modspec_gpu(cfg, sig, utts, rir=None, max_frames=4096):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", MODSPEC_SETS)
 def test_modspec_gpu_vs_reference_golden(name):
+    meta, sig, ref, _ = load_golden(name)
+    res = _modspec_gpu(_cfg(meta["opts"]), sig, meta["utts"])
+    for u in meta["utts"]:
+        f64, f32 = res[u]
+        assert f64.shape == ref[u].shape, u
+        scale = np.maximum(1.0, np.abs(ref[u]))
+        assert np.max(np.abs(f64 - ref[u]) / scale) <= TOL, (name, u, np.max(np.abs(f64 - ref[u]) / scale))
+        np.testing.assert_allclose(f32, np.round(ref[u], 3).astype(np.float32), rtol=0, atol=1.0011e-3 * scale.max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", COMPLEX_SETS)
+def test_modspec_complex_gpu_vs_reference_golden(name):
     meta, sig, ref, _ = load_golden(name)
     res = _modspec_gpu(_cfg(meta["opts"]), sig, meta["utts"])
     for u in meta["utts"]:
@@ -129,6 +170,28 @@ def test_modspec_cli_writes_reference_arks(tmp_path):
     assert list(ark) == meta["utts"]
     scp_keys = [l.split()[0] for l in open(out + ".scp")]
     assert scp_keys == meta["utts"]
+    for u in meta["utts"]:
+        q = np.round(ref[u], 3).astype(np.float32)
+        assert ark[u].shape == q.shape
+        assert np.abs(ark[u] - q).max() <= 1.0011e-3 * max(1.0, np.abs(ref[u]).max())
+
+
+@pytest.mark.gpu
+def test_modspec_complex_cli_writes_reference_arks(tmp_path):
+    from scipy.io import wavfile
+    from speech_recognition_tools_amd.featgen.computeModulationSpectrum import get_args, get_feats
+    from speech_recognition_tools_amd.featgen.features import read_ark
+    meta, sig, ref, _ = load_golden("modspec_complex")
+    scp = tmp_path / "wav.scp"
+    with open(scp, "w") as f:
+        for u in meta["utts"]:
+            p = tmp_path / (u + ".wav")
+            wavfile.write(str(p), 16000, sig[u])
+            f.write("%s %s\n" % (u, p))
+    out = str(tmp_path / "modspec_c")
+    get_feats(get_args([str(scp), out, "--complex_modulation"]))
+    ark = read_ark(out + ".ark")
+    assert list(ark) == meta["utts"]
     for u in meta["utts"]:
         q = np.round(ref[u], 3).astype(np.float32)
         assert ark[u].shape == q.shape
