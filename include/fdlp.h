@@ -342,6 +342,9 @@ typedef struct fdlp_job_stats {
   double read_wait_seconds;    /* consumer waiting for the reader threads       */
   double write_seconds;        /* writer thread busy (ark/scp/len)              */
   double slot_wait_seconds;    /* consumer waiting for a free batch slot        */
+  double plan_seconds;         /* fdlp_plan_create (part of setup)              */
+  double pinned_seconds;       /* pinned host buffers of the first slot (setup); the
+                                  other slots are pinned by a helper thread      */
 } fdlp_job_stats;
 int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_path, const char* outfile,
                  const fdlp_job_opts* opts, fdlp_job_stats* stats);

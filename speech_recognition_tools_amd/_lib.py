@@ -97,7 +97,8 @@ class FdlpJobStatsC(ctypes.Structure):
     _fields_ = [
         ("n_lines", c_i64), ("n_done", c_i64), ("n_skipped", c_i64), ("n_frames_out", c_i64),
         ("n_samples", c_i64), ("seconds", c_dbl), ("setup_seconds", c_dbl), ("read_wait_seconds", c_dbl),
-        ("write_seconds", c_dbl), ("slot_wait_seconds", c_dbl),
+        ("write_seconds", c_dbl), ("slot_wait_seconds", c_dbl), ("plan_seconds", c_dbl),
+        ("pinned_seconds", c_dbl),
     ]
 
 

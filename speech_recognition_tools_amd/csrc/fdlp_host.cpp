@@ -12,7 +12,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <sys/uio.h>
+#include <unistd.h>
+
 #include <climits>
+#include <algorithm>
 #include <new>
 #include <string>
 #include <vector>
@@ -350,6 +354,72 @@ int fdlp_ark_write(fdlp_ark_writer* w, const char* utt, const float* mat, int32_
     return w->failed = true, fdlp::fail(FDLP_E_IO, "scp write failed");
   return FDLP_OK;
 }
+
+}  // extern "C" (the batch writer below is internal C++)
+
+namespace fdlp {
+int ark_write_batch(fdlp_ark_writer* w, const ArkItem* items, size_t n, int32_t cols) {
+  if (!w || (n && !items) || cols < 0) return fail(FDLP_E_INVALID, "ark_write_batch: bad args");
+  if (fflush(w->ark) != 0) return w->failed = true, fail(FDLP_E_IO, "ark write failed");
+  const int fd = fileno(w->ark);
+  off_t pos = lseek(fd, 0, SEEK_CUR);
+  if (pos < 0) return w->failed = true, fail(FDLP_E_IO, "ark seek failed");
+  constexpr size_t kChunk = 512;  // utterances per writev (2 iovecs each, <= IOV_MAX)
+  std::vector<char> hdr;
+  std::vector<size_t> hoff;
+  std::vector<struct iovec> iov;
+  for (size_t i0 = 0; i0 < n; i0 += kChunk) {
+    const size_t i1 = std::min(n, i0 + kChunk);
+    hdr.clear();
+    hoff.clear();
+    for (size_t i = i0; i < i1; ++i) {  // "<utt> \0BFM \4<rows>\4<cols>"
+      const ArkItem& it = items[i];
+      if (!it.id || it.rows < 0 || ((int64_t)it.rows * cols > 0 && !it.data))
+        return w->failed = true, fail(FDLP_E_INVALID, "ark_write_batch: bad item");
+      hoff.push_back(hdr.size());
+      hdr.insert(hdr.end(), it.id, it.id + strlen(it.id));
+      hdr.push_back(' ');
+      const char tag[] = {'\0', 'B', 'F', 'M', ' ', 4};
+      hdr.insert(hdr.end(), tag, tag + 6);
+      const char* r = (const char*)&it.rows;
+      hdr.insert(hdr.end(), r, r + 4);
+      hdr.push_back(4);
+      const char* c = (const char*)&cols;
+      hdr.insert(hdr.end(), c, c + 4);
+    }
+    hoff.push_back(hdr.size());
+    iov.clear();
+    size_t total = 0;
+    for (size_t i = i0; i < i1; ++i) {
+      const size_t hl = hoff[i - i0 + 1] - hoff[i - i0];
+      iov.push_back({hdr.data() + hoff[i - i0], hl});
+      const size_t dl = sizeof(float) * (size_t)items[i].rows * (size_t)cols;
+      if (dl) iov.push_back({(void*)items[i].data, dl});
+      // scp: the offset of the matrix (just after "<utt> ")
+      if (w->scp && fprintf(w->scp, "%s %s:%lld\n", items[i].id, w->ark_abs.c_str(),
+                            (long long)(pos + (off_t)total + (off_t)strlen(items[i].id) + 1)) < 0)
+        return w->failed = true, fail(FDLP_E_IO, "scp write failed");
+      total += hl + dl;
+    }
+    size_t k = 0;  // writev until every iovec is out (it may write partially)
+    while (k < iov.size()) {
+      const int cnt = (int)std::min<size_t>(iov.size() - k, IOV_MAX);
+      const ssize_t got = writev(fd, iov.data() + k, cnt);
+      if (got < 0) return w->failed = true, fail(FDLP_E_IO, "ark write failed");
+      size_t left = (size_t)got;
+      while (k < iov.size() && left >= iov[k].iov_len) left -= iov[k++].iov_len;
+      if (left) {
+        iov[k].iov_base = (char*)iov[k].iov_base + left;
+        iov[k].iov_len -= left;
+      }
+    }
+    pos += (off_t)total;
+  }
+  return FDLP_OK;
+}
+}  // namespace fdlp
+
+extern "C" {
 
 // Closes the files and renames <ark>.tmp / <scp>.tmp to their final names (a JOB's outputs appear
 // only once complete); after a write failure the temporaries are removed instead.

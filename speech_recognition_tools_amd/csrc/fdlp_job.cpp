@@ -292,6 +292,7 @@ struct Slot {
   hipEvent_t ev_in = nullptr;    // its PCM is on the device
   hipEvent_t ev_comp = nullptr;  // its features are computed
   bool busy = false;           // in flight or not yet written
+  bool pinned = false;         // h_pcm / h_out allocated (by the pinning thread)
 };
 
 struct JobState {
@@ -302,6 +303,8 @@ struct JobState {
   int err = FDLP_OK;
   std::string err_msg;
   std::vector<Slot>* slots = nullptr;
+  int pin_err = FDLP_OK;       // pinning thread failure
+  std::string pin_msg;
 };
 
 int grow_pinned(void** p, size_t* cap, size_t need) {
@@ -364,9 +367,60 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
 
   fdlp_config c = *cfg;
   c.max_frames = std::max(1, o->batch_frames);
+  // pinned slot sizes for a full int16 batch: the plan's hop (features.py:135, :104, :174) and rows per frame
+  const double ov = 1.0 - c.overlap_fraction;
+  const int hop0 = (int)((double)c.srate / (1.0 / (ov * c.fduration)));
+  const size_t pin_smp = (size_t)c.max_frames * (size_t)(std::max(hop0, 1) + 1);
+  const size_t pin_rows = (size_t)c.max_frames * (size_t)((int64_t)hop0 * c.frate / std::max(1, c.srate) + 2);
+  const size_t pin_out_bytes = pin_rows * (size_t)std::max(1, c.nfilters) * sizeof(float);
+  std::vector<Slot> slots(3);
+  std::vector<size_t> hout_cap(slots.size(), 0);  // bytes of each slot's pinned output
+  JobState js;
+  js.slots = &slots;
+  // pinning thread: page-locking the three slots' host buffers (~0.4 GB) overlaps the plan creation and
+  // the first reads; slot k becomes usable when slots[k].pinned is set
+  std::thread pinner([&] {
+    for (size_t k = 0; k < slots.size(); ++k) {
+      const double t0 = now_s();
+      void* hp = nullptr;
+      size_t cap = 0;
+      float* ho = nullptr;
+      int e = grow_pinned(&hp, &cap, pin_smp * sizeof(int16_t));
+      if (e == FDLP_OK && hipHostMalloc((void**)&ho, pin_out_bytes, hipHostMallocDefault) != hipSuccess)
+        e = fail(FDLP_E_NOMEM, "pinned host allocation failed");
+      std::lock_guard<std::mutex> g(js.m);
+      if (k == 0) stats.pinned_seconds = now_s() - t0;
+      if (e != FDLP_OK) {
+        if (hp) (void)hipHostFree(hp);
+        if (ho) (void)hipHostFree(ho);
+        js.pin_err = e;
+        js.pin_msg = fdlp::last_error_slot();
+        js.cv.notify_all();
+        return;
+      }
+      slots[k].h_pcm = hp;
+      slots[k].pcm_cap = cap;
+      slots[k].h_out = ho;
+      hout_cap[k] = pin_out_bytes;
+      slots[k].pinned = true;
+      js.cv.notify_all();
+    }
+  });
+  auto join_pinner = [&] {
+    if (pinner.joinable()) pinner.join();
+  };
   fdlp_plan* plan = nullptr;
+  const double t_plan = now_s();
   int rc = fdlp_plan_create(&c, device, &plan);
-  if (rc != FDLP_OK) return rc;
+  stats.plan_seconds = now_s() - t_plan;
+  if (rc != FDLP_OK) {
+    join_pinner();
+    for (auto& sl : slots) {
+      if (sl.h_pcm) (void)hipHostFree(sl.h_pcm);
+      if (sl.h_out) (void)hipHostFree(sl.h_out);
+    }
+    return rc;
+  }
   int32_t B = 0;
   fdlp_plan_out_dim(plan, &B);
 
@@ -378,16 +432,14 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   fdlp_ark_writer* ark = nullptr;
   int16_t* d_noise = nullptr;
   double* d_cmvn = nullptr;
-  std::vector<Slot> slots(3);
   CopyPool copies(4);  // before cleanup(): drained there before the pinned buffers are freed
-  JobState js;
-  js.slots = &slots;
   std::string len_text;
   std::thread writer;
   int32_t sr_seen = -1;  // 'sr' of the last successful read (:139; NameError before the first one)
 
   auto cleanup = [&](int code) -> int {
     std::string keep = code != FDLP_OK ? fdlp::last_error_slot() : std::string();
+    join_pinner();
     if (writer.joinable()) {
       {
         std::lock_guard<std::mutex> g(js.m);
@@ -475,13 +527,17 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
         msg = "device batch failed";
       }
       const double tb = now_s();
-      for (size_t i = 0; i < d.ids.size() && err == FDLP_OK; ++i) {
-        const int64_t r0 = d.rows[i], r1 = d.rows[i + 1];
-        if (fdlp_ark_write(ark, d.ids[i].c_str(), sl.h_out + r0 * B, (int32_t)(r1 - r0), B) != FDLP_OK) {
+      if (err == FDLP_OK) {
+        std::vector<fdlp::ArkItem> items(d.ids.size());
+        for (size_t i = 0; i < d.ids.size(); ++i) {
+          const int64_t r0 = d.rows[i], r1 = d.rows[i + 1];
+          items[i] = {d.ids[i].c_str(), sl.h_out + r0 * B, (int32_t)(r1 - r0)};
+          if (o->write_len) len_text += d.ids[i] + " " + std::to_string(r1 - r0) + "\n";  // :235-236
+        }
+        if (fdlp::ark_write_batch(ark, items.data(), items.size(), B) != FDLP_OK) {
           err = FDLP_E_IO;
           msg = fdlp::last_error_slot();
         }
-        if (o->write_len) len_text += d.ids[i] + " " + std::to_string(r1 - r0) + "\n";  // :235-236
       }
       write_busy += now_s() - tb;
       {
@@ -511,9 +567,10 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   auto acquire_slot = [&](int k) -> int {
     const double ta = now_s();
     std::unique_lock<std::mutex> g(js.m);
-    js.cv.wait(g, [&] { return !slots[k].busy || js.err != FDLP_OK; });
+    js.cv.wait(g, [&] { return (!slots[k].busy && slots[k].pinned) || js.err != FDLP_OK || js.pin_err != FDLP_OK; });
     stats.slot_wait_seconds += now_s() - ta;
     if (js.err != FDLP_OK) return fail(js.err, js.err_msg);
+    if (js.pin_err != FDLP_OK) return fail(js.pin_err, js.pin_msg);
     return FDLP_OK;
   };
   JOB_TRY(acquire_slot(slot_i));
@@ -575,17 +632,11 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     return acquire_slot(slot_i);
   };
 
-  std::vector<size_t> hout_cap(slots.size(), 0);  // bytes of each slot's pinned output
-  {  // pinned and device buffers of a full int16 batch, allocated up front (growth stays possible)
-    int32_t N_, hop = 0, nl_, kk_, oh_;
-    fdlp_plan_info(plan, &N_, &hop, &nl_, &kk_, &oh_);
-    const size_t smp = (size_t)c.max_frames * (size_t)(hop + 1);
-    const size_t rows = (size_t)c.max_frames * (size_t)((int64_t)hop * c.frate / std::max(1, c.srate) + 2);
+  {  // device buffers of a full int16 batch, allocated up front (growth stays possible); the pinned host
+     // buffers come from the pinning thread started before the plan (acquire_slot waits for them)
+    const size_t smp = pin_smp, rows = pin_rows;
     for (size_t k = 0; k < slots.size(); ++k) {
       Slot& sl = slots[k];
-      JOB_TRY(grow_pinned(&sl.h_pcm, &sl.pcm_cap, smp * sizeof(int16_t)));
-      JOB_HIP(hipHostMalloc((void**)&sl.h_out, rows * B * sizeof(float), hipHostMallocDefault));
-      hout_cap[k] = rows * B * sizeof(float);
       JOB_TRY(grow_device(&sl.d_pcm, &sl.d_pcm_cap, smp * sizeof(int16_t), s));
       JOB_TRY(grow_device((void**)&sl.d_out, &sl.out_cap, rows * B * sizeof(float), s));
     }

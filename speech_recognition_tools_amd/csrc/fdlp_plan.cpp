@@ -10,6 +10,7 @@
 #include <cmath>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/fdlp.h"
@@ -87,18 +88,26 @@ std::vector<double> fbank_cochlear(int nf, int nfft, int srate, double om_w, dou
   std::vector<double> fl = linspace(0.0, fmax, ncol);
   for (auto& v : fl) v = bark(v);
   std::vector<double> W((size_t)nf * ncol);
-  for (int i = 0; i < nf; ++i) {
-    const double fc = cf[i];
-    const double a = fixed == 1 ? alp : alp * exp(-0.1 * fc);
-    for (int j = 0; j < ncol; ++j) {
-      const double d = fl[j] - fc;
-      double v;
-      if (d <= -om_w / 2.0) v = pow(10.0, a * (d + om_w / 2.0));
-      else if (d > -om_w / 2.0 && d < om_w / 2.0) v = 1.0;
-      else v = pow(10.0, -bet * (d - om_w / 2.0));
-      W[(size_t)i * ncol + j] = v;
+  auto rows = [&](int i0, int i1) {
+    for (int i = i0; i < i1; ++i) {
+      const double fc = cf[i];
+      const double a = fixed == 1 ? alp : alp * exp(-0.1 * fc);
+      for (int j = 0; j < ncol; ++j) {
+        const double d = fl[j] - fc;
+        double v;
+        if (d <= -om_w / 2.0) v = pow(10.0, a * (d + om_w / 2.0));
+        else if (d > -om_w / 2.0 && d < om_w / 2.0) v = 1.0;
+        else v = pow(10.0, -bet * (d - om_w / 2.0));
+        W[(size_t)i * ncol + j] = v;
+      }
     }
-  }
+  };
+  // ~2M pow calls for the recipes' 80 x 24001 taps: rows on a few threads (same values per element)
+  const int nt = std::max(1, std::min({8, nf, (int)std::thread::hardware_concurrency()}));
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(rows, nf * t / nt, nf * (t + 1) / nt);
+  rows(0, nf / nt);
+  for (auto& x : th) x.join();
   *ncol_out = ncol;
   return W;
 }
@@ -543,18 +552,66 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   if (!p->real_fft && !split_four_step(p->nfft_c, &p->d1, &p->d2))
     PLAN_FAIL(FDLP_E_INVALID, "frame length int(srate*fduration) has no supported 2/3/5/7 four-step split");
 
+  // skirt tables and the DFT twiddle tables need only the configuration: built on helper threads while
+  // the filterbank is computed (plan creation is on the CLI's critical path)
+  bool sk_ok = false;
+  std::thread sk_thread([&] { sk_ok = !p->cplx && skirt_tables(c, p->B, p->N, p->nfft, &p->sk); });
+  const int N1 = p->d1.n, N2 = p->d2.n, NC = p->nfft_c;
+  std::vector<double> tw1(2 * (size_t)N1 * N2), post(2 * (size_t)p->N), rtw(2 * (size_t)std::max(1, p->N / 2));
+  std::vector<double2> om1, om2;
+  std::thread tw_thread([&] {
+    const int N = p->N;
+    const long double PI = 3.141592653589793238462643383279502884L;
+    for (int k1 = 0; k1 < N1; ++k1)
+      for (int n2 = 0; n2 < N2; ++n2) {
+        const long long q = ((long long)k1 * n2) % NC;
+        const long double ang = -2.0L * PI * (long double)q / (long double)NC;
+        tw1[2 * ((size_t)k1 * N2 + n2)] = (double)cosl(ang);
+        tw1[2 * ((size_t)k1 * N2 + n2) + 1] = (double)sinl(ang);
+      }
+    for (int k = 0; k < N / 2; ++k) {
+      const long double ang = -2.0L * PI * (long double)k / (long double)N;
+      rtw[2 * k] = (double)cosl(ang);
+      rtw[2 * k + 1] = (double)sinl(ang);
+    }
+    for (int k = 0; k < N; ++k) {
+      const long double ang = -PI * (long double)k / (2.0L * (long double)N);
+      post[2 * k] = (double)cosl(ang);
+      post[2 * k + 1] = (double)sinl(ang);
+    }
+    auto omega = [&](int n) {
+      std::vector<double2> om(n);
+      for (int q = 0; q < n; ++q) {
+        const long double ang = -2.0L * PI * (long double)q / (long double)n;
+        om[q] = make_double2((double)cosl(ang), (double)sinl(ang));
+      }
+      return om;
+    };
+    om1 = omega(N1);
+    om2 = omega(N2);
+  });
+  auto join_helpers = [&] {
+    if (sk_thread.joinable()) sk_thread.join();
+    if (tw_thread.joinable()) tw_thread.join();
+  };
   // filterbank (:49-63)
   if (c.fbank_kind == FDLP_FBANK_MEL) {
     p->fbank_host = fbank_mel(p->B, p->nfft, c.srate, c.warp_fact, &p->ncol);
   } else if (c.fbank_kind == FDLP_FBANK_COCHLEAR) {
     p->fbank_host = fbank_cochlear(p->B, p->nfft, c.srate, c.om_w, c.alp, c.fixed, c.bet, c.warp_fact, &p->ncol);
   } else {
+    join_helpers();
     PLAN_FAIL(FDLP_E_INVALID, "Invalid type of filter bank, use mel or cochlear with proper configuration");
   }
   const int width = p->cplx ? p->L : p->N;  // taps of filt = fbank[j, :-1]
-  if (p->ncol - 1 != width)  // filt (ncol-1 taps) * cos_trans[i, :] (N, or L ifft bins) must broadcast (:190-191)
+  if (p->ncol - 1 != width) {  // filt (ncol-1 taps) * cos_trans[i, :] (N, or L ifft bins) must broadcast (:190-191)
+    join_helpers();
     PLAN_FAIL(FDLP_E_INVALID, "filterbank width nfft/2 does not match the frame length (reference broadcast error)");
-  if (p->cplx && p->nlags > p->L) PLAN_FAIL(FDLP_E_INVALID, "complex_modulation: order + 2 exceeds the ifft bins");
+  }
+  if (p->cplx && p->nlags > p->L) {
+    join_helpers();
+    PLAN_FAIL(FDLP_E_INVALID, "complex_modulation: order + 2 exceeds the ifft bins");
+  }
   std::vector<double> dense((size_t)p->B * p->N);  // rows of N (cplx: the L taps, zeros beyond)
   p->lo.assign(p->B, 0);
   p->hi.assign(p->B, 0);
@@ -574,7 +631,8 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
     p->hi[j] = hi;
   }
 
-  p->sk_avail = !p->cplx && skirt_tables(c, p->B, p->N, p->nfft, &p->sk);
+  join_helpers();
+  p->sk_avail = sk_ok;
   p->vs_avail = p->sk_avail && p->sk.fl_C > 0 && fdlp::vsweep_chains(p->sk.fl_C) > 0 &&
                 fdlp::vsweep_lanes_lags(p->nlags) > 0;
   p->ac_path = !p->sk_avail || getenv("FDLP_AUTOCORR_DIRECT") ? FDLP_AC_DIRECT
@@ -613,35 +671,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   std::vector<double> env_cos(p->env_nfft);
   for (int q = 0; q < p->env_nfft; ++q)
     env_cos[q] = (double)cosl(2.0L * (long double)M_PI * (long double)q / (long double)p->env_nfft);
-  const int N1 = p->d1.n, N2 = p->d2.n, N = p->N, NC = p->nfft_c;
-  std::vector<double> tw1(2 * (size_t)N1 * N2), post(2 * (size_t)N), rtw(2 * (size_t)std::max(1, N / 2));
-  const long double PI = 3.141592653589793238462643383279502884L;
-  for (int k1 = 0; k1 < N1; ++k1)
-    for (int n2 = 0; n2 < N2; ++n2) {
-      const long long q = ((long long)k1 * n2) % NC;
-      const long double ang = -2.0L * PI * (long double)q / (long double)NC;
-      tw1[2 * ((size_t)k1 * N2 + n2)] = (double)cosl(ang);
-      tw1[2 * ((size_t)k1 * N2 + n2) + 1] = (double)sinl(ang);
-    }
-  for (int k = 0; k < N / 2; ++k) {
-    const long double ang = -2.0L * PI * (long double)k / (long double)N;
-    rtw[2 * k] = (double)cosl(ang);
-    rtw[2 * k + 1] = (double)sinl(ang);
-  }
-  for (int k = 0; k < N; ++k) {
-    const long double ang = -PI * (long double)k / (2.0L * (long double)N);
-    post[2 * k] = (double)cosl(ang);
-    post[2 * k + 1] = (double)sinl(ang);
-  }
-  auto omega = [&](int n) {
-    std::vector<double2> om(n);
-    for (int q = 0; q < n; ++q) {
-      const long double ang = -2.0L * PI * (long double)q / (long double)n;
-      om[q] = make_double2((double)cosl(ang), (double)sinl(ang));
-    }
-    return om;
-  };
-  const std::vector<double2> om1 = omega(N1), om2 = omega(N2);
+  const int N = p->N;
 
   p->max_frames = c.max_frames;
   // the fused autocorr+LPC-tail kernel measured slower (35.7 vs 25.5+3.9 ms, r01); opt-in only
