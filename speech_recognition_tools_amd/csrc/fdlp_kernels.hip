@@ -371,11 +371,23 @@ __device__ __forceinline__ void bfly_c(double2 (&v)[R]) {
   }
 }
 
+// LDS slot of element (pos, col) of COLS = 8 interleaved columns.  SWZ: the column index XORed with
+// g(pos mod 8) = ((pos & 1) << 2) | ((pos & 7) >> 1), so 8 consecutive positions of one column (the
+// row pass's coalesced load order) land in 8 different 16-byte bank groups, while the 8 columns of one
+// position still fill its 128 bytes (the stage reads' lane groups pair positions p and p + 2 on
+// complementary column halves; g keeps bit 2 equal for p and p + 2, so they stay disjoint).
+template <bool SWZ>
+__device__ __forceinline__ int lslot(int pos, int col) {
+  if constexpr (SWZ) return pos * 8 + (col ^ (((pos & 1) << 2) | ((pos & 7) >> 1)));
+  else return pos * 8 + col;
+}
+
 // One Stockham stage (radix R, Ns = product of the radices before it) of COLS interleaved length-N
 // columns in LDS; om = the N roots omega_N^q.
-template <int N, int COLS, int NT, int Ns, int R>
+template <int N, int COLS, int NT, int Ns, int R, bool SWZ = false>
 __device__ __forceinline__ void st_stage_c(const double2* __restrict__ in, double2* __restrict__ out,
                                            const double2* __restrict__ om) {
+  static_assert(!SWZ || COLS == 8, "swizzle of 8 columns");
   constexpr int NB = N / R, TOT = NB * COLS, ITER = (TOT + NT - 1) / NT, TW0 = N / (Ns * R);
 #pragma unroll
   for (int it = 0; it < ITER; ++it) {
@@ -386,22 +398,25 @@ __device__ __forceinline__ void st_stage_c(const double2* __restrict__ in, doubl
     double2 v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const double2 x = in[(j + r * NB) * COLS + col];
+      const double2 x = SWZ ? in[lslot<SWZ>(j + r * NB, col)] : in[(j + r * NB) * COLS + col];
       v[r] = (r == 0 || Ns == 1) ? x : cmul(x, om[TW0 * k * r]);
     }
     bfly_c<R>(v);
     const int idxD = jq * Ns * R + k;
 #pragma unroll
-    for (int r = 0; r < R; ++r) out[(idxD + r * Ns) * COLS + col] = v[r];
+    for (int r = 0; r < R; ++r) {
+      if constexpr (SWZ) out[lslot<SWZ>(idxD + r * Ns, col)] = v[r];
+      else out[(idxD + r * Ns) * COLS + col] = v[r];
+    }
   }
 }
 
 // full length-N DFT of COLS columns, radices R0 R1 ...; returns the buffer holding the result
-template <int N, int COLS, int NT, int Ns, int R0, int... Rs>
+template <int N, int COLS, int NT, bool SWZ, int Ns, int R0, int... Rs>
 __device__ __forceinline__ double2* lds_dft_c(double2* a, double2* b, const double2* om) {
-  st_stage_c<N, COLS, NT, Ns, R0>(a, b, om);
+  st_stage_c<N, COLS, NT, Ns, R0, SWZ>(a, b, om);
   __syncthreads();
-  if constexpr (sizeof...(Rs) > 0) return lds_dft_c<N, COLS, NT, Ns * R0, Rs...>(b, a, om);
+  if constexpr (sizeof...(Rs) > 0) return lds_dft_c<N, COLS, NT, SWZ, Ns * R0, Rs...>(b, a, om);
   else return b;
 }
 
@@ -411,16 +426,16 @@ template <>
 struct DctRadices1<100> {
   template <int COLS, int NT>
   __device__ static double2* run(double2* a, double2* b, const double2* om) {
-    return lds_dft_c<100, COLS, NT, 1, 4, 5, 5>(a, b, om);
+    return lds_dft_c<100, COLS, NT, false, 1, 4, 5, 5>(a, b, om);
   }
 };
 template <int N2>
 struct DctRadices2;
 template <>
 struct DctRadices2<120> {
-  template <int COLS, int NT>
+  template <int COLS, int NT, bool SWZ = false>
   __device__ static double2* run(double2* a, double2* b, const double2* om) {
-    return lds_dft_c<120, COLS, NT, 1, 4, 2, 3, 5>(a, b, om);
+    return lds_dft_c<120, COLS, NT, SWZ, 1, 4, 2, 3, 5>(a, b, om);
   }
 };
 
@@ -483,7 +498,7 @@ __global__ __launch_bounds__(256) void frames_dft1_c_kernel(DevConsts c, const v
 }
 
 // rows k1 of pair pp (pp, N1 - pp): slots r (< COLS/2) and r + COLS/2
-template <int N1, int N2, int COLS, bool TWF = true>
+template <int N1, int N2, int COLS, bool TWF = true, bool SWZ = true>
 __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const double2* __restrict__ z,
                                                          const double2* __restrict__ om2, double inv_scale_div,
                                                          double* __restrict__ dct, int nframes) {
@@ -521,10 +536,10 @@ __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const doub
     const int k1 = slot_row(row);
     double2 v = make_double2(0.0, 0.0);
     if (k1 >= 0) v = z[((int64_t)f * N1 + k1) * N2 + n2];
-    bufA[n2 * COLS + row] = v;
+    bufA[lslot<SWZ>(n2, row)] = v;
   }
   __syncthreads();
-  const double2* res = DctRadices2<N2>::template run<COLS, NT>(bufA, bufB, oms);
+  const double2* res = DctRadices2<N2>::template run<COLS, NT, SWZ>(bufA, bufB, oms);
   const double2* post = (const double2*)c.post;
   const double2* rtw = (const double2*)c.rtw;
   constexpr int M = N1 * N2;
@@ -536,11 +551,11 @@ __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const doub
     const int k1 = slot_row(row);
     if (k1 < 0) continue;
     const int k = k1 + N1 * k2;
-    const double2 V = res[k2 * COLS + row];
+    const double2 V = res[lslot<SWZ>(k2, row)];
     const int k1m = k1 == 0 ? 0 : N1 - k1;
     const int k2m = k1 == 0 ? (k2 == 0 ? 0 : N2 - k2) : N2 - 1 - k2;
     const int rm = k1m == k1 ? row : (row < HALF ? row + HALF : row - HALF);
-    const double2 W = res[k2m * COLS + rm];
+    const double2 W = res[lslot<SWZ>(k2m, rm)];
     const double2 E = make_double2(0.5 * (V.x + W.x), 0.5 * (V.y - W.y));
     const double2 O = make_double2(0.5 * (V.y + W.y), -0.5 * (V.x - W.x));
     double2 rt, w1, w2;
@@ -2743,8 +2758,12 @@ hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const 
     dim3 grid((N1 / 2 + 1 + kDftCols / 2 - 1) / (kDftCols / 2), nframes);
     static const bool table_tw = getenv("FDLP_DCT_TABLE_TW") != nullptr;  // A/B knob: full post/rtw tables
     const dim3 g1(xcd_grid(grid.x * nframes));
+    static const bool no_swz = getenv("FDLP_DCT_NOSWZ") != nullptr;  // A/B knob: unswizzled LDS columns
     if (table_tw)
       hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, false>), g1, dim3(256), 0, s, c, z, om2, div, dct, nframes);
+    else if (no_swz)
+      hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, true, false>), g1, dim3(256), 0, s, c, z, om2, div, dct,
+                         nframes);
     else
       hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, true>), g1, dim3(256), 0, s, c, z, om2, div, dct, nframes);
     return hipGetLastError();
