@@ -1915,6 +1915,58 @@ __device__ __forceinline__ void cep_terms16(double& a0, double& a1, double& a2, 
   fmac_bcast<15>(a3, kc, v[15]);
 }
 
+// 16 alpha values alpha[OFF - j] (j < 16, byte offsets from the lane's LDS address `addr`) as single
+// ds_read_b64: 2 LDS cycles per wave-instruction, where the compiler's merged ds_read2_b64 takes 8 for
+// two (MI355X_MICROARCH.md LDS table).  The asm results look ready to the compiler, so the caller
+// waits (lgkm_wait) before the FMAs that read them.
+template <int OFF, int J = 0>
+__device__ __forceinline__ void lds_load16(double (&v)[16], uint32_t addr) {
+  if constexpr (J < 16) {
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v[J]) : "v"(addr), "i"(8 * (OFF - J)) : "memory");
+    lds_load16<OFF, J + 1>(v, addr);
+  }
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory"); }
+
+__device__ __forceinline__ void cep_fma16(double& a0, double& a1, double& a2, double& a3, double kc,
+                                          const double (&v)[16]) {
+  fmac_bcast<0>(a0, kc, v[0]);
+  fmac_bcast<1>(a1, kc, v[1]);
+  fmac_bcast<2>(a2, kc, v[2]);
+  fmac_bcast<3>(a3, kc, v[3]);
+  fmac_bcast<4>(a0, kc, v[4]);
+  fmac_bcast<5>(a1, kc, v[5]);
+  fmac_bcast<6>(a2, kc, v[6]);
+  fmac_bcast<7>(a3, kc, v[7]);
+  fmac_bcast<8>(a0, kc, v[8]);
+  fmac_bcast<9>(a1, kc, v[9]);
+  fmac_bcast<10>(a2, kc, v[10]);
+  fmac_bcast<11>(a3, kc, v[11]);
+  fmac_bcast<12>(a0, kc, v[12]);
+  fmac_bcast<13>(a1, kc, v[13]);
+  fmac_bcast<14>(a2, kc, v[14]);
+  fmac_bcast<15>(a3, kc, v[15]);
+}
+
+// The window blocks w = WI .. W-1 of one cepstrum block (CB < 0): block w's 16 alpha values were issued
+// before this call (va); block w + 1's are issued before block w's FMAs (double buffer), and the wait
+// before the FMAs leaves those 16 in flight (LDS operations complete in order).
+template <int W, int WI>
+__device__ __forceinline__ void cep_window(double& a0, double& a1, double& a2, double& a3, const double (&kc)[W],
+                                           double (&va)[16], double (&vb)[16], uint32_t addr) {
+  if constexpr (WI < W) {
+    if constexpr (WI + 1 < W) {
+      lds_load16<16 * (WI + 1) + 15>(vb, addr);
+      lgkm_wait<15>();  // all of block WI's loads (and the first of WI + 1's) have landed
+    } else {
+      lgkm_wait<0>();
+    }
+    cep_fma16(a0, a1, a2, a3, kc[WI], va);
+    cep_window<W, WI + 1>(a0, a1, a2, a3, kc, vb, va, addr);
+  }
+}
+
 // In-block part of the cepstrum recurrence for coefficient b0 + KK: lane KK finishes c_{b0+KK},
 // DPP row_newbcast hands it to the row, the later lanes of the block fold it in.
 // a_kg is read from la only up to amax (beyond it a is zero: the reference pads alpha with zeros).
@@ -2415,35 +2467,14 @@ __global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(Lpc
         const double inv_n = 1.0 / (double)(n > 0 ? n : 1);
         double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
         asm volatile("s_nop 1");  // kc[0] was just written: DPP reads need 2 wait states
-        // the next block-term's 16 alpha values are loaded before this one's FMAs (double buffer)
-        double v[2][16];
-        const double* al0 = la + n - b0 + 16;  // k = b0 - 16 (w + 1) + j: alpha_{n-k} = al0[16 w - j]
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v[0][j] = al0[-j];
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-          if (w + 1 < W) {
-#pragma unroll
-            for (int j = 0; j < 16; ++j) v[(w + 1) & 1][j] = al0[16 * (w + 1) - j];
-          }
-          const double* vv = v[w & 1];
-          fmac_bcast<0>(a0, kc[w], vv[0]);
-          fmac_bcast<1>(a1, kc[w], vv[1]);
-          fmac_bcast<2>(a2, kc[w], vv[2]);
-          fmac_bcast<3>(a3, kc[w], vv[3]);
-          fmac_bcast<4>(a0, kc[w], vv[4]);
-          fmac_bcast<5>(a1, kc[w], vv[5]);
-          fmac_bcast<6>(a2, kc[w], vv[6]);
-          fmac_bcast<7>(a3, kc[w], vv[7]);
-          fmac_bcast<8>(a0, kc[w], vv[8]);
-          fmac_bcast<9>(a1, kc[w], vv[9]);
-          fmac_bcast<10>(a2, kc[w], vv[10]);
-          fmac_bcast<11>(a3, kc[w], vv[11]);
-          fmac_bcast<12>(a0, kc[w], vv[12]);
-          fmac_bcast<13>(a1, kc[w], vv[13]);
-          fmac_bcast<14>(a2, kc[w], vv[14]);
-          fmac_bcast<15>(a3, kc[w], vv[15]);
-        }
+        // k = b0 - 16 (w + 1) + j: alpha_{n-k} = la[n - b0 + 16 w + 16 - j]; the lane's base address is
+        // la + n - b0 + 1, so window block w reads byte offsets 8 (16 w + 15 - j)
+        double va[16], vb[16];
+        const uint32_t aaddr =
+            (uint32_t)(uintptr_t)((__attribute__((address_space(3))) double*)(la + n - b0 + 1));
+        lgkm_wait<0>();  // nothing else (scalar loads complete out of order) may share the counted waits
+        lds_load16<15>(va, aaddr);
+        cep_window<W, 0>(a0, a1, a2, a3, kc, va, vb, aaddr);
         double acc = (a0 + a1) + (a2 + a3);
         double mine = 0.0;
         cep_block_step<0>(b0, Mc, l, gg, inv_n, la, n, acc, mine, p);
