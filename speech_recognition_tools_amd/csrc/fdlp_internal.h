@@ -61,7 +61,7 @@ struct DevConsts {
   const double* hamming;   // [N]   np.hamming(N)
   const double* weights;   // [3, M] mask (:94-103), lifter (:195-196), gamma (:197-198); 1.0 if absent
   const double* env_cos;   // [env_nfft] cos(2*pi*q/env_nfft)
-  const double* env_win;   // [kk, 2] (hanning(kk)[t], hamming(kk)[t]) interleaved (:205)
+  const double* env_win;   // [kk, 2] (hanning(kk)[t] / hamming(kk)[t], 1.0) interleaved (:205)
   const double* tw1;       // [N1 * N2] four-step twiddles exp(-2*pi*i*n2*k1/(N1*N2)) (complex)
   const double* post;      // [N] complex exp(-i*pi*k/(2N)) (Makhoul post-twiddle)
   const double* rtw;       // [N/2] complex exp(-2*pi*i*k/N) (real-FFT unpacking; real_fft only)

@@ -16,6 +16,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 
 #include <algorithm>
 #include <atomic>
@@ -52,7 +53,9 @@ struct Utt {
   std::shared_ptr<std::vector<double>> f64;    // otherwise (scipy's dtype, converted exactly as numpy does)
 };
 
-// memcpy jobs (utterance samples -> the pinned batch buffer) on a few threads; a job keeps its source alive
+// memcpy jobs (utterance samples -> the pinned batch buffer) on a few threads; a job keeps its source
+// alive.  The consumer's copies are handed over in groups (kGroup utterances, or fewer at a wait), so
+// the hand-off costs one lock and one wake-up per group, not per utterance.  Single producer.
 class CopyPool {
  public:
   explicit CopyPool(int n) {
@@ -67,19 +70,18 @@ class CopyPool {
     for (auto& t : th_) t.join();
   }
   void submit(int tag, void* dst, const void* src, size_t n, std::shared_ptr<void> keep) {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      q_.push_back(Job{tag, dst, src, n, std::move(keep)});
-      ++pending_[tag];
-    }
-    cv_.notify_one();
+    if (!stage_.empty() && stage_.front().tag != tag) push_stage();
+    stage_.push_back(Job{tag, dst, src, n, std::move(keep)});
+    if (stage_.size() >= kGroup) push_stage();
   }
   void wait(int tag) {
+    push_stage();
     std::unique_lock<std::mutex> g(m_);
     done_.wait(g, [&] { return pending_[tag] == 0; });
   }
 
  private:
+  static constexpr size_t kGroup = 16;
   struct Job {
     int tag;
     void* dst;
@@ -87,28 +89,42 @@ class CopyPool {
     size_t n;
     std::shared_ptr<void> keep;
   };
+  void push_stage() {
+    if (stage_.empty()) return;
+    const int tag = stage_.front().tag;
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back(std::move(stage_));
+      ++pending_[tag];
+    }
+    stage_ = std::vector<Job>();
+    cv_.notify_one();
+  }
   void run() {
     for (;;) {
-      Job j;
+      std::vector<Job> grp;
       {
         std::unique_lock<std::mutex> g(m_);
         cv_.wait(g, [&] { return stop_ || !q_.empty(); });
         if (q_.empty()) return;
-        j = std::move(q_.front());
+        grp = std::move(q_.front());
         q_.pop_front();
       }
-      memcpy(j.dst, j.src, j.n);
-      j.keep.reset();
+      for (auto& j : grp) {
+        memcpy(j.dst, j.src, j.n);
+        j.keep.reset();
+      }
       {
         std::lock_guard<std::mutex> g(m_);
-        --pending_[j.tag];
+        --pending_[grp.front().tag];
       }
       done_.notify_all();
     }
   }
   std::mutex m_;
   std::condition_variable cv_, done_;
-  std::deque<Job> q_;
+  std::deque<std::vector<Job>> q_;
+  std::vector<Job> stage_;  // the producer's group being filled (no lock: single producer)
   int pending_[8] = {0};
   bool stop_ = false;
   std::vector<std::thread> th_;
@@ -130,10 +146,18 @@ bool read_file(const std::string& path, int64_t offset, std::vector<uint8_t>& ou
       out.resize(8 + got);
     }
   } else if (ok) {
-    out.clear();
-    uint8_t buf[1 << 16];
-    size_t n;
-    while ((n = fread(buf, 1, sizeof buf, f)) > 0) out.insert(out.end(), buf, buf + n);
+    // one read of the whole file into a buffer of its size (no growth copies); anything past the
+    // size fstat saw (a file still growing) is appended in chunks
+    struct stat sb;
+    const size_t sz = fstat(fileno(f), &sb) == 0 && S_ISREG(sb.st_mode) ? (size_t)sb.st_size : 0;
+    out.resize(sz);
+    size_t got = sz ? fread(out.data(), 1, sz, f) : 0;
+    out.resize(got);
+    if (got == sz) {
+      uint8_t buf[1 << 16];
+      size_t n;
+      while ((n = fread(buf, 1, sizeof buf, f)) > 0) out.insert(out.end(), buf, buf + n);
+    }
     ok = !ferror(f);
   }
   fclose(f);
@@ -211,6 +235,9 @@ void read_entry(const std::string& line, Utt& u) {
 }
 
 // ---- ordered read-ahead pool -------------------------------------------------------------------
+// Readers run up to `depth` entries ahead of the consumer.  Wake-ups are targeted: a reader is woken
+// only if one is parked on the depth limit, the consumer only when the entry it waits for is in, so
+// the per-utterance cost of the hand-off is a lock, not a broadcast to every thread.
 class Reader {
  public:
   Reader(std::vector<std::string> lines, int threads, int depth) : lines_(std::move(lines)), depth_(depth) {
@@ -230,16 +257,23 @@ class Reader {
   // entry i (blocks until read); the caller releases it with done(i)
   Utt& get(size_t i) {
     std::unique_lock<std::mutex> g(m_);
-    cv_done_.wait(g, [&] { return ready_[i] != 0; });
+    if (!ready_[i]) {
+      want_ = i;
+      cv_done_.wait(g, [&] { return ready_[i] != 0; });
+      want_ = SIZE_MAX;
+    }
     return slots_[i];
   }
   void done(size_t i) {
+    Utt dead;
+    bool wake;
     {
       std::lock_guard<std::mutex> g(m_);
-      slots_[i] = Utt();
+      dead = std::move(slots_[i]);  // freed outside the lock
       consumed_ = i + 1;
+      wake = parked_ > 0;
     }
-    cv_.notify_all();
+    if (wake) cv_.notify_all();
   }
 
  private:
@@ -248,24 +282,32 @@ class Reader {
       size_t i;
       {
         std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [&] { return stop_ || (next_ < lines_.size() && next_ < consumed_ + depth_); });
+        if (!(stop_ || (next_ < lines_.size() && next_ < consumed_ + depth_))) {
+          ++parked_;
+          cv_.wait(g, [&] { return stop_ || (next_ < lines_.size() && next_ < consumed_ + depth_) || next_ >= lines_.size(); });
+          --parked_;
+        }
         if (stop_ || next_ >= lines_.size()) return;
         i = next_++;
       }
       Utt u;
       read_entry(lines_[i], u);
+      bool wake;
       {
         std::lock_guard<std::mutex> g(m_);
         slots_[i] = std::move(u);
         ready_[i] = 1;
+        wake = want_ == i;
       }
-      cv_done_.notify_all();
+      if (wake) cv_done_.notify_one();
     }
   }
   std::vector<std::string> lines_;
   std::vector<Utt> slots_;
   std::vector<char> ready_;
   size_t next_ = 0, consumed_ = 0, depth_;
+  size_t want_ = SIZE_MAX;  // the entry the consumer waits for
+  int parked_ = 0;          // readers waiting on the depth limit
   bool stop_ = false;
   std::mutex m_;
   std::condition_variable cv_, cv_done_;
@@ -363,7 +405,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   }
   stats.n_lines = (int64_t)lines.size();
 
-  Reader reader(lines, std::max(1, o->io_threads), 64);  // reading starts while the plan is built
+  Reader reader(lines, std::max(1, o->io_threads), 512);  // reading starts while the plan is built
 
   fdlp_config c = *cfg;
   c.max_frames = std::max(1, o->batch_frames);
@@ -562,6 +604,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     int kind = FDLP_PCM_I16;
   } pend;
   int slot_i = 0;
+  int32_t ramp = std::max(64, c.max_frames / 8);  // frames of the current batch (see the loop)
 
   // waits until the slot's previous batch is written, then makes it the current one
   auto acquire_slot = [&](int k) -> int {
@@ -676,7 +719,12 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     if (o->progress_name) printf("%s: Computing Features for file: %s\n", o->progress_name, u.id.c_str());  // :185
     // a batch is one PCM kind and at most max_frames frames
     int32_t cap = c.max_frames;
-    if (!pend.ids.empty() && (pend.frames + F > cap || pend.kind != kind)) JOB_TRY(flush());
+    // batches ramp up (max_frames / 8, doubling per batch) so the device starts after the first few
+    // reads and the pipeline fill is short; steady state runs at max_frames
+    if (!pend.ids.empty() && (pend.frames + F > std::min(cap, ramp) || pend.kind != kind)) {
+      JOB_TRY(flush());
+      ramp = ramp < cap ? 2 * ramp : ramp;
+    }
     if (F > cap) {  // an utterance longer than a batch: a bigger plan (the Python drop-in does the same)
       JOB_HIP(hipStreamSynchronize(s));
       {

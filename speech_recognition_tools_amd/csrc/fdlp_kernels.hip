@@ -500,8 +500,10 @@ __global__ __launch_bounds__(256) void frames_dft1_c_kernel(DevConsts c, const v
 // rows k1 of pair pp (pp, N1 - pp): slots r (< COLS/2) and r + COLS/2
 template <int N1, int N2, int COLS, bool TWF = true, bool SWZ = true>
 __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const double2* __restrict__ z,
-                                                         const double2* __restrict__ om2, double inv_scale_div,
+                                                         const double2* __restrict__ om2, double scale2,
                                                          double* __restrict__ dct, int nframes) {
+  // scale2 = 2 / sqrt(2N): dct(.) / np.sqrt(2N) (:178) as one multiplication (within an ulp of the
+  // reference's division; no fp64 division per coefficient)
   constexpr int NT = 256, HALF = COLS / 2;
   __shared__ double2 bufA[N2 * COLS], bufB[N2 * COLS], oms[N2];
   __shared__ double2 pw1[N1], pw2[N2], rw1[N1], rw2[N2];  // factored twiddles (TWF)
@@ -573,8 +575,8 @@ __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const doub
     const double2 t = cmul(rt, O);
     const double2 V1 = make_double2(E.x + t.x, E.y + t.y);
     const double2 V2 = make_double2(E.x - t.x, E.y - t.y);
-    dct[(int64_t)f * N + k] = 2.0 * (w1.x * V1.x - w1.y * V1.y) / inv_scale_div;
-    dct[(int64_t)f * N + k + M] = 2.0 * (w2.x * V2.x - w2.y * V2.y) / inv_scale_div;
+    dct[(int64_t)f * N + k] = (w1.x * V1.x - w1.y * V1.y) * scale2;
+    dct[(int64_t)f * N + k + M] = (w2.x * V2.x - w2.y * V2.y) * scale2;
   }
 }
 
@@ -629,7 +631,7 @@ struct LpcTail {
   const double* weights;  // [3, M]
   const double* env_cos;  // [env_nfft]
   int env_nfft;
-  const double* env_win;  // [kk, 2]
+  const double* env_win;  // [kk, 2]: (hanning / hamming ratio, 1.0)
 };
 
 constexpr int kTS64 = 4;  // envelope samples per lane (kk <= 256)
@@ -713,7 +715,7 @@ __device__ void lpc_tail64(const LpcTail& T, double* la, double* lr, double* env
       cprev = ccur;
       ccur = nxt;
     }
-    env[t] = (exp(sum) * T.env_win[2 * t]) / T.env_win[2 * t + 1];
+    env[t] = exp(sum) * T.env_win[2 * t];
   }
 }
 
@@ -1840,7 +1842,7 @@ struct LpcEnvArgs {
   const double* r;
   const double* weights;  // [3, M]
   const double* env_cos;  // [env_nfft]
-  const double* env_win;  // [kk, 2]
+  const double* env_win;  // [kk, 2]: (hanning / hamming ratio, 1.0)
   double* env;            // [items, kk]
   double* a_out;          // nullable [items, p+1]
   double* gg_out;         // nullable [items]
@@ -2561,9 +2563,9 @@ __global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(Lpc
         for (int q = 0; q < kEnvChunk; ++q) {
           const int u = l + 16 * (q0 + q);
           if (2 * u > H) continue;
-          if (u < A.kk) out[u] = (exp(se[q] + so[q]) * A.env_win[2 * u]) / A.env_win[2 * u + 1];
+          if (u < A.kk) out[u] = exp(se[q] + so[q]) * A.env_win[2 * u];
           const int t2 = H - u;
-          if (t2 != u && t2 < A.kk) out[t2] = (exp(se[q] - so[q]) * A.env_win[2 * t2]) / A.env_win[2 * t2 + 1];
+          if (t2 != u && t2 < A.kk) out[t2] = exp(se[q] - so[q]) * A.env_win[2 * t2];
         }
       }
     }
@@ -2661,9 +2663,9 @@ __global__ __launch_bounds__(64) void lpc_env_kernel(LpcEnvArgs A) {
     for (int q = 0; q < TS; ++q) {
       const int u = l + 16 * q;
       if (2 * u > H) continue;
-      if (u < A.kk) out[u] = (exp(se[q] + so[q]) * A.env_win[2 * u]) / A.env_win[2 * u + 1];
+      if (u < A.kk) out[u] = exp(se[q] + so[q]) * A.env_win[2 * u];
       const int t2 = H - u;
-      if (t2 != u && t2 < A.kk) out[t2] = (exp(se[q] - so[q]) * A.env_win[2 * t2]) / A.env_win[2 * t2 + 1];
+      if (t2 != u && t2 < A.kk) out[t2] = exp(se[q] - so[q]) * A.env_win[2 * t2];
     }
   }
 }
@@ -2789,14 +2791,15 @@ hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const 
     dim3 grid((N1 / 2 + 1 + kDftCols / 2 - 1) / (kDftCols / 2), nframes);
     static const bool table_tw = getenv("FDLP_DCT_TABLE_TW") != nullptr;  // A/B knob: full post/rtw tables
     const dim3 g1(xcd_grid(grid.x * nframes));
+    const double sc2 = 2.0 / div;
     static const bool no_swz = getenv("FDLP_DCT_NOSWZ") != nullptr;  // A/B knob: unswizzled LDS columns
     if (table_tw)
-      hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, false>), g1, dim3(256), 0, s, c, z, om2, div, dct, nframes);
+      hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, false>), g1, dim3(256), 0, s, c, z, om2, sc2, dct, nframes);
     else if (no_swz)
-      hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, true, false>), g1, dim3(256), 0, s, c, z, om2, div, dct,
+      hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, true, false>), g1, dim3(256), 0, s, c, z, om2, sc2, dct,
                          nframes);
     else
-      hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, true>), g1, dim3(256), 0, s, c, z, om2, div, dct, nframes);
+      hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, true>), g1, dim3(256), 0, s, c, z, om2, sc2, dct, nframes);
     return hipGetLastError();
   }
   if (c.real_fft) {

@@ -667,7 +667,10 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   else PLAN_FAIL(FDLP_E_INVALID, "unknown analysis window");
   const std::vector<double> hann_k = cos_window(p->kk, 0.5, 0.5), hamm_k = cos_window(p->kk, 0.54, 0.46);
   std::vector<double> env_win(2 * (size_t)p->kk);
-  for (int t = 0; t < p->kk; ++t) { env_win[2 * t] = hann_k[t]; env_win[2 * t + 1] = hamm_k[t]; }
+  // ms[0:kk] * np.hanning(kk) / window(kk) (computeFDLPSpectrogram.py:205) as one multiplication by the
+  // ratio, rounded once here (a 1-ulp difference from the reference's two roundings; no fp64 division
+  // per envelope sample on the device).  [2t + 1] stays 1.0 for the kernels that still divide.
+  for (int t = 0; t < p->kk; ++t) { env_win[2 * t] = hann_k[t] / hamm_k[t]; env_win[2 * t + 1] = 1.0; }
   std::vector<double> env_cos(p->env_nfft);
   for (int q = 0; q < p->env_nfft; ++q)
     env_cos[q] = (double)cosl(2.0L * (long double)M_PI * (long double)q / (long double)p->env_nfft);
