@@ -7,6 +7,7 @@ mkdir -p gpurun_out
 PYTEST_ARGS="tests -m gpu -x -q --timeout 300 --timeout-method thread" BENCH_ARGS="--no-cpu-baseline" \
   bash scripts/gpu_check.sh || exit $?
 bash scripts/ab_trace.sh - || exit $?
+[ -n "${SKIP_CLI:-}" ] && exit 0
 for bf in 2048 8192; do
   timeout -k 10 300 python benchmarks/cli_throughput.py --utts 8192 --workers 4 8 --runners native \
     --batch-frames $bf > gpurun_out/cli_$bf.jsonl 2>&1 || { tail -20 gpurun_out/cli_$bf.jsonl; exit 5; }

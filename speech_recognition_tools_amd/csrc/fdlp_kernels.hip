@@ -383,42 +383,74 @@ __device__ __forceinline__ int lslot(int pos, int col) {
 }
 
 // One Stockham stage (radix R, Ns = product of the radices before it) of COLS interleaved length-N
-// columns in LDS; om = the N roots omega_N^q.
-template <int N, int COLS, int NT, int Ns, int R, bool SWZ = false>
+// columns in LDS; om = the N roots omega_N^q.  IP (in place, in == out): every thread reads and
+// transforms all its butterflies first, then a barrier, then the writes; one buffer instead of two,
+// so twice the workgroups fit a CU's LDS (same arithmetic, bit-identical results).
+template <int N, int COLS, int NT, int Ns, int R, bool SWZ = false, bool IP = false>
 __device__ __forceinline__ void st_stage_c(const double2* __restrict__ in, double2* __restrict__ out,
                                            const double2* __restrict__ om) {
   static_assert(!SWZ || COLS == 8, "swizzle of 8 columns");
   constexpr int NB = N / R, TOT = NB * COLS, ITER = (TOT + NT - 1) / NT, TW0 = N / (Ns * R);
+  const double2* src = in;
+  double2* dst = out;
+  if constexpr (IP) src = out;  // the caller passes the one buffer as out
+  auto slot = [&](int pos, int col) { return SWZ ? lslot<SWZ>(pos, col) : pos * COLS + col; };
+  double2 v[IP ? ITER : 1][R];
 #pragma unroll
   for (int it = 0; it < ITER; ++it) {
     const int b = (int)threadIdx.x + it * NT;
     if (TOT % NT != 0 && b >= TOT) break;
     const int col = b % COLS, j = b / COLS;
     const int k = j % Ns, jq = j / Ns;
-    double2 v[R];
+    double2 (&w)[R] = v[IP ? it : 0];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const double2 x = SWZ ? in[lslot<SWZ>(j + r * NB, col)] : in[(j + r * NB) * COLS + col];
-      v[r] = (r == 0 || Ns == 1) ? x : cmul(x, om[TW0 * k * r]);
+      const double2 x = src[slot(j + r * NB, col)];
+      w[r] = (r == 0 || Ns == 1) ? x : cmul(x, om[TW0 * k * r]);
     }
-    bfly_c<R>(v);
-    const int idxD = jq * Ns * R + k;
+    bfly_c<R>(w);
+    if constexpr (!IP) {
+      const int idxD = jq * Ns * R + k;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if constexpr (SWZ) out[lslot<SWZ>(idxD + r * Ns, col)] = v[r];
-      else out[(idxD + r * Ns) * COLS + col] = v[r];
+      for (int r = 0; r < R; ++r) dst[slot(idxD + r * Ns, col)] = w[r];
+    }
+  }
+  if constexpr (IP) {
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int b = (int)threadIdx.x + it * NT;
+      if (TOT % NT != 0 && b >= TOT) break;
+      const int col = b % COLS, j = b / COLS;
+      const int k = j % Ns, jq = j / Ns;
+      const int idxD = jq * Ns * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) dst[slot(idxD + r * Ns, col)] = v[it][r];
     }
   }
 }
 
 // full length-N DFT of COLS columns, radices R0 R1 ...; returns the buffer holding the result
-template <int N, int COLS, int NT, bool SWZ, int Ns, int R0, int... Rs>
+// (IP: a only, b unused)
+template <int N, int COLS, int NT, bool SWZ, bool IP, int Ns, int R0, int... Rs>
 __device__ __forceinline__ double2* lds_dft_c(double2* a, double2* b, const double2* om) {
-  st_stage_c<N, COLS, NT, Ns, R0, SWZ>(a, b, om);
-  __syncthreads();
-  if constexpr (sizeof...(Rs) > 0) return lds_dft_c<N, COLS, NT, SWZ, Ns * R0, Rs...>(b, a, om);
-  else return b;
+  if constexpr (IP) {
+    st_stage_c<N, COLS, NT, Ns, R0, SWZ, true>(a, a, om);
+    __syncthreads();
+    if constexpr (sizeof...(Rs) > 0) return lds_dft_c<N, COLS, NT, SWZ, true, Ns * R0, Rs...>(a, b, om);
+    else return a;
+  } else {
+    st_stage_c<N, COLS, NT, Ns, R0, SWZ>(a, b, om);
+    __syncthreads();
+    if constexpr (sizeof...(Rs) > 0) return lds_dft_c<N, COLS, NT, SWZ, false, Ns * R0, Rs...>(b, a, om);
+    else return b;
+  }
 }
+
+#ifndef FDLP_DCT_IP
+#define FDLP_DCT_IP 1  // in-place Stockham stages in the specialised DCT kernels (0: ping-pong buffers)
+#endif
+constexpr bool kDctIP = FDLP_DCT_IP != 0;
 
 template <int N1>
 struct DctRadices1;
@@ -426,7 +458,7 @@ template <>
 struct DctRadices1<100> {
   template <int COLS, int NT>
   __device__ static double2* run(double2* a, double2* b, const double2* om) {
-    return lds_dft_c<100, COLS, NT, false, 1, 4, 5, 5>(a, b, om);
+    return lds_dft_c<100, COLS, NT, false, kDctIP, 1, 4, 5, 5>(a, b, om);
   }
 };
 template <int N2>
@@ -435,7 +467,7 @@ template <>
 struct DctRadices2<120> {
   template <int COLS, int NT, bool SWZ = false>
   __device__ static double2* run(double2* a, double2* b, const double2* om) {
-    return lds_dft_c<120, COLS, NT, SWZ, 1, 4, 2, 3, 5>(a, b, om);
+    return lds_dft_c<120, COLS, NT, SWZ, kDctIP, 1, 4, 2, 3, 5>(a, b, om);
   }
 };
 
@@ -446,7 +478,7 @@ __global__ __launch_bounds__(256) void frames_dft1_c_kernel(DevConsts c, const v
                                                             const double2* __restrict__ om1,
                                                             double2* __restrict__ z, int nframes) {
   constexpr int NT = 256;
-  __shared__ double2 bufA[N1 * COLS], bufB[N1 * COLS], oms[N1], twb[N2];
+  __shared__ double2 bufA[N1 * COLS], bufB[kDctIP ? 1 : N1 * COLS], oms[N1], twb[N2];
   // 1-D grid, XCD-mapped: the column blocks of a frame run on one XCD (their z rows share L2 lines)
   constexpr int NBX = (N2 + COLS - 1) / COLS;
   const int it0 = xcd_item();
@@ -505,7 +537,7 @@ __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const doub
   // scale2 = 2 / sqrt(2N): dct(.) / np.sqrt(2N) (:178) as one multiplication (within an ulp of the
   // reference's division; no fp64 division per coefficient)
   constexpr int NT = 256, HALF = COLS / 2;
-  __shared__ double2 bufA[N2 * COLS], bufB[N2 * COLS], oms[N2];
+  __shared__ double2 bufA[N2 * COLS], bufB[kDctIP ? 1 : N2 * COLS], oms[N2];
   __shared__ double2 pw1[N1], pw2[N2], rw1[N1], rw2[N2];  // factored twiddles (TWF)
   // 1-D grid, XCD-mapped: the row-pair blocks of a frame run on one XCD, so the 32-B runs they store
   // into each D line (k = k1 + N1 k2: 4 consecutive k1 per block) merge in that XCD's L2
