@@ -1234,14 +1234,23 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
       if (q < kWin) xa[q] = pos < b ? x : 0.0;
     }
     __syncthreads();
-    for (int st = (lb - b + kWin) >> 6; st < kWin / 64; ++st) {
+    // st unrolled, so each step's first live tile tmin is a constant: its MFMAs and their LDS reads are
+    // branch-free (the reads issue together instead of one exposed LDS latency per MFMA)
+    const int st0 = (lb - b + kWin) >> 6;
+#pragma unroll
+    for (int st = 0; st < kWin / 64; ++st) {
+      if (st < st0) continue;
       const int w = 64 * st + 16 * kk_lane + i_lane;
       const double a = xa[w];
       // tile t reads B positions up to b - kWin + 64 st + 63 + 16 t; below b they are all zero
       const int tmin = (kWin - 64 * st - 48) >> 4;
+      double bv[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t)
-        if (t >= tmin) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, xb[w + 16 * t], acc[t], 0, 0, 0);
+        if (t >= tmin) bv[t] = xb[w + 16 * t];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (t >= tmin) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv[t], acc[t], 0, 0, 0);
     }
   }
   __syncthreads();
