@@ -3,7 +3,7 @@
 # sadhusamik/speech_recognition_tools (same options and outputs), running each JOB's
 # compute-fdlp-feats on an MI355X.  Extra options: --ngpu N (JOB n runs on GPU (n-1) mod N, with or
 # without a Kaldi $cmd launcher: the CLI gets --device_rr=JOB,N and picks the device before any GPU
-# call), --jobs_per_gpu K (without $cmd: at most N*K JOBs run at once; default 1).
+# call), --jobs_per_gpu K (without $cmd: at most N*K JOBs run at once; default 2).
 #
 #   make_FDLPspectrum_feats.sh [--opts] <data_dir> <feat_dir>
 # Inputs: <data_dir>/wav.scp or <data_dir>/segments.  Outputs: <data_dir>/feats.scp,
@@ -32,7 +32,7 @@ write_utt2num_frames=false
 lifter_config=
 check_for_segment="data/train"
 ngpu=1
-jobs_per_gpu=1
+jobs_per_gpu=2  # two JOBs per GPU overlap each other's latency-bound kernels
 compute_cmvn=false   # also write <data_dir>/cmvn.ark (global CMVN stats, fused on the device)
 seed=
 noise_seed=
