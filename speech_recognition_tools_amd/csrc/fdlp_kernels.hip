@@ -963,7 +963,7 @@ __device__ __forceinline__ void diag_sums(const dbl4* acc, double* ep, int nlags
 // [LB g, LB g + LB); its 16-term sums touch tiles LB/16 g .. LB/16 (g+1), which are written whole
 // into a padded lag-major image (rows = lags LB g - 15 .. LB g + LB + 14, stride 17).  LPL = 64/LB
 // lanes share a lag, each adding 16/LPL consecutive terms, and a DPP swap finishes the sum; the
-// first lane of each group calls emit(L, r_L).  ep holds (LB + 31) * 17 doubles.  Block = one wave.
+// first lane of each group calls emit(L, r_L) (or emit(g, L, r_L) if emit takes the block index).  ep holds (LB + 31) * 17 doubles.  Block = one wave.
 template <int NT, int LB, typename Emit>
 __device__ __forceinline__ void diag_blocks(const dbl4* acc, double* ep, int nlags, int lane, Emit emit) {
   static_assert(LB == 32 || LB == 64, "lag block");
@@ -998,7 +998,10 @@ __device__ __forceinline__ void diag_blocks(const dbl4* acc, double* ep, int nla
     for (int i = 0; i < 16 / LPL; ++i) sum += v[i];
     if constexpr (LPL == 2) sum += dpp_f64<0xB1>(sum);  // quad_perm [1,0,3,2]: partner lane
     const int L = LB * g + m;
-    if (part == 0 && L < nlags) emit(L, sum);
+    if (part == 0 && L < nlags) {
+      if constexpr (std::is_invocable_v<Emit, int, int, double>) emit(g, L, sum);
+      else emit(L, sum);
+    }
     wave_lds_sync();
   }
 }
@@ -1257,18 +1260,37 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
   double* ro = r + (int64_t)item * nlags;
   const double* uo = rup + (int64_t)item * nlags;
   if constexpr (VS) {
+    // the diagonal sums first (kept in registers: acc is dead afterwards), then the rows they are added
+    // to (lower / upper skirt snapshots, flat sum, partial chains of the flat parts above m1's) loaded
+    // for all of the lane's lags at once: one exposed memory latency per item instead of one per block
+    constexpr int kNB = (16 * NT + 31) / 32;
+    double sums[kNB];
+#pragma unroll
+    for (int g = 0; g < kNB; ++g) sums[g] = 0.0;
+    diag_blocks<NT, 32>(acc, xs, nlags, lane, [&](int g, int, double v) { sums[g] = v; });
     const double* fo = rflat + (int64_t)item * nlags;
-    // partial flat sums of the parts above the one holding m1 (at most kMaxFlatParts - 1)
     const int2 fb = c.fl_band[j];
-    const double* po[kMaxFlatParts - 1];
-    int np = 0;
-    for (int h = 0; h + 1 < c.fl_H; ++h)
-      if (fb.y >> h & 1) po[np++] = rpart + (((int64_t)f * (c.fl_H - 1) + h) * kMaxChains + fb.x) * nlags;
-    diag_blocks<NT, 32>(acc, xs, nlags, lane, [&](int L, double v) {
-      double fl = fo[L];
-      for (int q = 0; q < np; ++q) fl += po[q][L];
-      ro[L] = v + ro[L] + uo[L] + fl;
-    });
+    const int pmask = fb.y & ((1 << (c.fl_H - 1)) - 1);  // parts h < fl_H - 1 added in increasing h
+    double rv[kNB], uv[kNB], fv[kNB];
+#pragma unroll
+    for (int g = 0; g < kNB; ++g) {
+      const int L = min(32 * g + (lane >> 1), nlags - 1);  // clamped: the loads are unconditional
+      rv[g] = ro[L];
+      uv[g] = uo[L];
+      fv[g] = fo[L];
+    }
+    if (pmask) {
+      for (int rest = pmask; rest; rest &= rest - 1) {
+        const double* po = rpart + (((int64_t)f * (c.fl_H - 1) + __builtin_ctz(rest)) * kMaxChains + fb.x) * nlags;
+#pragma unroll
+        for (int g = 0; g < kNB; ++g) fv[g] += po[min(32 * g + (lane >> 1), nlags - 1)];
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < kNB; ++g) {
+      const int L = 32 * g + (lane >> 1);
+      if ((lane & 1) == 0 && L < nlags) ro[L] = sums[g] + rv[g] + uv[g] + fv[g];
+    }
   } else {
     diag_blocks<NT, 32>(acc, xs, nlags, lane, [&](int L, double v) { ro[L] = v + ro[L] + uo[L]; });
   }
