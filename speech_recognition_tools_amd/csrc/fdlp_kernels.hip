@@ -2228,13 +2228,16 @@ __device__ __forceinline__ void contig_durbin(double (&A)[S], double (&B)[S], do
 #ifndef FDLP_D8_CHAINS
 #define FDLP_D8_CHAINS 4  // 2 or 4
 #endif
+#ifndef FDLP_D8_NEWTON
+#define FDLP_D8_NEWTON 2  // Newton steps after v_rcp_f64 for 1/E
+#endif
 template <int S>
 __device__ __forceinline__ void c8_step(double (&A)[S], const double (&Bs)[S], double (&Bd)[S],
                                         const double (&R1)[S], double& part, double& E, bool first) {
   const double acc = sum8(part);  // r_k + sum_i a_i r_{k-i}
   double rE = __builtin_amdgcn_rcp(E);
-  rE = fma(rE, fma(-E, rE, 1.0), rE);
-  rE = fma(rE, fma(-E, rE, 1.0), rE);
+#pragma unroll
+  for (int it = 0; it < FDLP_D8_NEWTON; ++it) rE = fma(rE, fma(-E, rE, 1.0), rE);
   const double kappa = -acc * rE;
   const double zs = __builtin_amdgcn_update_dpp(0.0, Bs[S - 1], 0x111, 0xF, 0xF, true);  // row_shr:1
   const double z0 = first ? 0.0 : zs;
