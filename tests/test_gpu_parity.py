@@ -311,3 +311,28 @@ def test_torch_op_matches_plan_compute():
     torch.cuda.synchronize()
     assert got.shape == (int(rows[-1]), 80) and got.dtype == torch.float32
     assert torch.equal(got, want)
+
+
+def test_batches_in_flight_on_streams_match_serial():
+    """Three plans featurising three batches concurrently on three HIP streams (bench.py --inflight)
+    give bit-identical features to one plan computing the batches in turn."""
+    from speech_recognition_tools_amd import FdlpPlan, FeatureConfig, PyRandom
+    rng = np.random.default_rng(9)
+    lens = [int(v) for v in rng.integers(16000, 120000, size=64)]
+    pcm = torch.from_numpy(np.clip(rng.standard_normal(sum(lens)) * 2000, -32768, 32767).astype(np.int16)).cuda()
+    plans = [FdlpPlan(FeatureConfig.wsj(), device=0, max_frames=512) for _ in range(3)]
+    nj = sum(plans[0].geometry(T)[0] - 1 for T in lens)
+    jits = [PyRandom(s).randbits2(nj) for s in (1, 2, 3)]
+    ref = []
+    for k in range(3):
+        _, _, o64 = plans[0].compute(pcm, lens, jits[k], want_f64=True)
+        torch.cuda.synchronize()
+        ref.append(o64.cpu().numpy())
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    res = []
+    for k in range(3):
+        with torch.cuda.stream(streams[k]):
+            res.append(plans[k].compute(pcm, lens, jits[k], want_f64=True)[2])
+    torch.cuda.synchronize()
+    for k in range(3):
+        np.testing.assert_array_equal(res[k].cpu().numpy(), ref[k])
