@@ -235,7 +235,8 @@ void read_entry(const std::string& line, Utt& u) {
 }
 
 // ---- ordered read-ahead pool -------------------------------------------------------------------
-// Readers run up to `depth` entries ahead of the consumer.  Wake-ups are targeted: a reader is woken
+// Readers run up to `depth` entries and about kAheadBytes of file data ahead of the consumer (at least
+// one entry, however large).  Wake-ups are targeted: a reader is woken
 // only if one is parked on the depth limit, the consumer only when the entry it waits for is in, so
 // the per-utterance cost of the hand-off is a lock, not a broadcast to every thread.
 class Reader {
@@ -243,6 +244,7 @@ class Reader {
   Reader(std::vector<std::string> lines, int threads, int depth) : lines_(std::move(lines)), depth_(depth) {
     slots_.resize(lines_.size());
     ready_.assign(lines_.size(), 0);
+    bytes_.assign(lines_.size(), 0);
     for (int t = 0; t < std::max(1, threads); ++t) th_.emplace_back([this] { run(); });
   }
   ~Reader() {
@@ -270,6 +272,7 @@ class Reader {
     {
       std::lock_guard<std::mutex> g(m_);
       dead = std::move(slots_[i]);  // freed outside the lock
+      ahead_bytes_ -= bytes_[i];
       consumed_ = i + 1;
       wake = parked_ > 0;
     }
@@ -278,13 +281,16 @@ class Reader {
 
  private:
   void run() {
+    auto may_start = [&] {
+      return next_ < lines_.size() && next_ < consumed_ + depth_ && (ahead_bytes_ < kAheadBytes || next_ == consumed_);
+    };
     for (;;) {
       size_t i;
       {
         std::unique_lock<std::mutex> g(m_);
-        if (!(stop_ || (next_ < lines_.size() && next_ < consumed_ + depth_))) {
+        if (!(stop_ || may_start())) {
           ++parked_;
-          cv_.wait(g, [&] { return stop_ || (next_ < lines_.size() && next_ < consumed_ + depth_) || next_ >= lines_.size(); });
+          cv_.wait(g, [&] { return stop_ || may_start() || next_ >= lines_.size(); });
           --parked_;
         }
         if (stop_ || next_ >= lines_.size()) return;
@@ -292,10 +298,13 @@ class Reader {
       }
       Utt u;
       read_entry(lines_[i], u);
+      const size_t nb = (u.raw ? u.raw->size() : 0) + (u.f64 ? u.f64->size() * sizeof(double) : 0);
       bool wake;
       {
         std::lock_guard<std::mutex> g(m_);
         slots_[i] = std::move(u);
+        bytes_[i] = nb;
+        ahead_bytes_ += nb;
         ready_[i] = 1;
         wake = want_ == i;
       }
@@ -307,6 +316,9 @@ class Reader {
   std::vector<char> ready_;
   size_t next_ = 0, consumed_ = 0, depth_;
   size_t want_ = SIZE_MAX;  // the entry the consumer waits for
+  static constexpr size_t kAheadBytes = size_t(256) << 20;
+  std::vector<size_t> bytes_;  // file data held by each read entry
+  size_t ahead_bytes_ = 0;     // held by entries read and not yet consumed
   int parked_ = 0;          // readers waiting on the depth limit
   bool stop_ = false;
   std::mutex m_;
