@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--ks", type=int, nargs="+", default=[1, 2, 3])
+    ap.add_argument("--stagger-cycles", type=int, default=0,
+                    help="stream k first spins k * this / K GPU cycles (torch.cuda._sleep) inside the timed region")
     a = ap.parse_args()
     import torch
     from bench import scp_list, utterance_pcm
@@ -46,6 +48,10 @@ def main():
                     plans[k].compute(pcm, lens, jit, out=outs[k])
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
+            if a.stagger_cycles:
+                for k in range(1, K):
+                    with torch.cuda.stream(streams[k]):
+                        torch.cuda._sleep(a.stagger_cycles * k // K)
             for s in range(a.steps):
                 for k in range(K):
                     with torch.cuda.stream(streams[k]):
