@@ -8,7 +8,18 @@ N x --utts entries (or U(1,30) s LibriSpeech-like entries, configs[4]) split int
 shards like utils/split_scp.pl (make_FDLPspectrum_feats.sh:135-157): every rank featurises its own
 shard with no collective (scaling is weak).  Prints ONE JSON line on rank 0.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config wsj|reverb] [--workload wsj|librispeech]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config wsj|reverb|chime4] [--workload wsj|librispeech|reverb]
+
+Configs (BASELINE.json configs[1..4]):
+  wsj      WSJ params (M 100, range 0..100), 4 s speech-like utterances (workload wsj, the headline);
+           --workload librispeech: U(1,30) s lengths (configs[4])
+  reverb   REVERB params (M 450, range 1..450), U(2,15) s utterances of two synthetic reverberant sets,
+           "1ch" (T60 0.7 s) and "8ch_beamformit" (T60 0.35 s, stronger direct path): speech-like signals
+           reverberated on the device by fdlp_reverb (addReverb, features.py:110-115) and stored as int16 PCM
+           like the recorded et_real WAVs (input synthesis, outside the timed region)
+  chime4   CHiME4 params (M 100, range 1..100), 4 s utterances mixed on the device with a synthetic babble
+           noise at 20 dB inside the timed kernels (--add_noise babble,20: features.py:24-31; the per-utterance
+           (offset, alpha) come from the numpy-legacy rand() replica like the reference's draws)
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
 With --gpus N > 1 and no launcher environment (WORLD_SIZE unset) bench.py starts the N rank processes
@@ -62,102 +73,219 @@ def utterance_pcm(entries):
 def scp_list(workload, world, utts, seconds, frames, frames_of):
     """The synthetic scp of the whole job: [(utt_id, T, seed)].
     wsj: world * utts utterances of `seconds` (configs[1]).  librispeech: lengths U(1, 30) s (seeded,
-    SURVEY.md 8(d) config 5) until the list holds world * frames analysis frames (so every rank's
-    contiguous shard is about `frames` frames, one device batch)."""
+    SURVEY.md 8(d) config 5); reverb: lengths U(2, 15) s (8(d) config 3), entries alternating between the
+    "1ch" and "8ch_beamformit" sets.  The U(a, b) lists grow until they hold world * frames analysis frames
+    (so every rank's contiguous shard is about `frames` frames, one device batch)."""
     if workload == "wsj":
         T = int(round(seconds * 16000))
         return [("wsj%06d" % i, T, 1000 + i) for i in range(world * utts)]
-    rs = np.random.RandomState(2000)
+    lo, hi, rseed, seed0 = {"librispeech": (1.0, 30.0, 2000, 5000), "reverb": (2.0, 15.0, 3000, 9000)}[workload]
+    rs = np.random.RandomState(rseed)
     out, fr = [], 0
     while True:
-        t = int(rs.uniform(1.0, 30.0) * 16000)
+        t = int(rs.uniform(lo, hi) * 16000)
         f = frames_of(t)
         if fr + f > world * frames:
             return out
-        out.append(("libri%06d" % len(out), t, 5000 + len(out)))
+        i = len(out)
+        name = "libri%06d" % i if workload == "librispeech" else "et_%s_%06d" % (REVERB_SETS[i & 1], i)
+        out.append((name, t, seed0 + i))
         fr += f
 
 
+REVERB_SETS = ("1ch", "8ch_beamformit")
+
+
+def synthetic_rir(kind, fs=16000):
+    """Synthetic room impulse response of a REVERB set: a unit direct path after
+    2.5 ms and an exponentially decaying Gaussian tail (60 dB over T60) whose energy sits `drr` dB below
+    the direct path, normalised to unit energy.  "1ch": T60 0.7 s, DRR 0 dB (a distant single
+    microphone); "8ch_beamformit": T60 0.35 s, DRR +8 dB (the beamformed array output is drier)."""
+    t60, drr_db, seed = {"1ch": (0.7, 0.0, 11), "8ch_beamformit": (0.35, 8.0, 12)}[kind]
+    rng = np.random.default_rng(seed)
+    R = int(t60 * fs)
+    d0 = int(0.0025 * fs)
+    n = np.arange(R, dtype=np.float64)
+    tail = rng.standard_normal(R) * np.exp(-6.907755278982137 * (n - d0) / (t60 * fs))
+    tail[:d0 + 16] = 0.0
+    tail *= np.sqrt(10.0 ** (-drr_db / 10.0) / np.sum(tail * tail))
+    h = tail
+    h[d0] = 1.0
+    return h / np.sqrt(np.sum(h * h))
+
+
+def reverb_pcm(entries, device):
+    """int16 PCM of REVERB-like entries: each set's speech-like signals go through fdlp_reverb on the device
+    with the set's synthetic RIR (full convolution + the reference's xcorr alignment, features.py:110-115),
+    then round/clip to int16 like a recorded WAV.  Returns (concatenated int16 numpy, lengths)."""
+    import torch
+    from speech_recognition_tools_amd.augment import reverb
+    parts = [None] * len(entries)
+    lens = [0] * len(entries)
+    for k, kind in enumerate(REVERB_SETS):
+        idx = [i for i in range(len(entries)) if (i & 1) == k]
+        if not idx:
+            continue
+        rir = torch.from_numpy(synthetic_rir(kind)).to(device)
+        for c0 in range(0, len(idx), 128):  # bounded device scratch (the convolution output is T + R - 1)
+            sub = [entries[i] for i in idx[c0:c0 + 128]]
+            sl = [t for _, t, _ in sub]
+            x = torch.from_numpy(utterance_pcm(sub)).to(device)
+            y, ol = reverb(x, sl, rir)
+            y = torch.clamp(torch.round(y), -32768, 32767).to(torch.int16).cpu().numpy()
+            off = np.concatenate([[0], np.cumsum(sl)])
+            for j, i in enumerate(idx[c0:c0 + 128]):
+                parts[i] = y[off[j]:off[j] + int(ol[j])]
+                lens[i] = int(ol[j])
+    return np.concatenate(parts), lens
+
+
+NOISE_SNR = 20.0
+
+
+def babble_noise(seconds=240.0, seed=77):
+    """Synthetic noises/babble.wav stand-in (the reference's noises/*.wav are absent):
+    six overlapped speech-like talkers, int16."""
+    T = int(seconds * 16000)
+    rng = np.random.default_rng(seed)
+    acc = np.zeros(T)
+    for _ in range(6):
+        acc += speech_like(T, rng).astype(np.float64)
+    acc *= 2500.0 / np.sqrt(np.mean(acc * acc))
+    return np.clip(np.round(acc), -32768, 32767).astype(np.int16)
+
+
+def noise_mix(pcm_host, lens, noise, snr, nprandom):
+    """(offsets, alphas) of add_noise_to_wav (features.py:24-31) for every utterance of a batch in scp
+    order, each offset from one np.random.rand() draw of `nprandom` (NpRandom: the numpy legacy stream)."""
+    from speech_recognition_tools_amd.augment import noise_params
+    offs = np.empty(len(lens), dtype=np.int64)
+    alps = np.empty(len(lens), dtype=np.float64)
+    o = 0
+    for i, T in enumerate(lens):
+        offs[i], alps[i] = noise_params(pcm_host[o:o + T], noise, snr, nprandom.rand())
+        o += T
+    return offs, alps
+
+
 def _cpu_worker(args):
-    cfg_name, utts, seed = args
+    cfg_name, utts, seed, noise, noise_seed = args
     os.environ["OMP_NUM_THREADS"] = "1"
     import random
     from oracle import fdlp_oracle as O
     orc = O.FdlpOracle(getattr(O.FdlpConfig, cfg_name)())
     rng = random.Random(seed)
+    nrng = np.random.RandomState(noise_seed)
     t0 = time.perf_counter()
     for x in utts:
+        if noise is not None:  # add_noise_to_wav (features.py:24-31), as the timed GPU path mixes
+            x = O.add_noise(x, noise, NOISE_SNR, nrng.rand())
         orc.utterance(x, rng)
     return time.perf_counter() - t0
 
 
-def cpu_baseline(cfg_name, T, workers, per_worker):
+def cpu_baseline(cfg_name, lens, workers, per_worker, noise=None):
     """The oracle (reference-equivalent fp64 numpy restatement, cpu_baseline kind "port") on a bounded
-    sample of the same workload, one process per core."""
-    sig = speech_like_batch(workers * per_worker, T, 4242)
-    jobs = [(cfg_name, [sig[w * per_worker + i] for i in range(per_worker)], 100 + w) for w in range(workers)]
+    sample of the same workload (the first workers x per_worker utterance lengths of it), one process per
+    core."""
+    n = workers * per_worker
+    lens = [lens[i % len(lens)] for i in range(n)]
+    rng = np.random.default_rng(4242)
+    sig = [speech_like(T, rng) for T in lens]
+    jobs = [(cfg_name, sig[w * per_worker:(w + 1) * per_worker], 100 + w, noise, 300 + w) for w in range(workers)]
     ctx = mp.get_context("fork")
     with ctx.Pool(workers) as pool:
         times = pool.map(_cpu_worker, jobs)
-    audio_h = workers * per_worker * T / 16000.0 / 3600.0
+    audio_h = sum(lens) / 16000.0 / 3600.0
     return dict(value=audio_h / max(times), unit="audio-hours/s", cores=workers, kind="port",
-                sample="%d x %.1f s synthetic utterances (%d per process), oracle/fdlp_oracle.py, "
-                       "OMP_NUM_THREADS=1, steady state (plan setup excluded), %.1f s wall" %
-                       (workers * per_worker, T / 16000.0, per_worker, max(times)))
+                sample="%d synthetic utterances of the %s workload (%.1f audio-s, %d per process%s), "
+                       "oracle/fdlp_oracle.py, OMP_NUM_THREADS=1, steady state (plan setup excluded), %.1f s wall" %
+                       (n, cfg_name, sum(lens) / 16000.0, per_worker,
+                        ", babble mixed at %g dB" % NOISE_SNR if noise is not None else "", max(times)))
 
 
-def _latest_pmc():
-    """The newest committed PMC summary (profiles/rNN*_pmc.json, written by scripts/round_evidence.sh)."""
+def _latest_pmc(config="wsj"):
+    """The newest committed PMC summary of a config (profiles/rNN*_pmc.json for wsj,
+    profiles/rNN*_<config>_pmc.json otherwise; written by scripts/round_evidence.sh)."""
     import glob
     c = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc.json")))
+    tagged = lambda f: any(("_%s_pmc" % k) in os.path.basename(f) for k in ("reverb", "chime4", "librispeech"))
+    c = [f for f in c if ((("_%s_pmc" % config) in os.path.basename(f)) if config != "wsj" else not tagged(f))]
     return c[-1] if c else None
 
 
 PMC_FILE = _latest_pmc()
-AC_KERNEL_PREFIX = {"structured": ("fdlp::ac_vsweep_kernel", "fdlp::ac_band_kernel"),
-                    "structured_mfma": ("fdlp::ac_sweep_kernel", "fdlp::ac_band_kernel"),
-                    "direct": ("fdlp::autocorr_kernel",)}
+# kernels of each timed stage (fdlp_stage_times), as rocprofv3 names them
+STAGE_KERNELS = {"dct": ("fdlp::frames_dft1", "fdlp::dft2_dct"),
+                 "autocorr": {"structured": ("fdlp::ac_vsweep_kernel", "fdlp::ac_band_kernel"),
+                              "structured_mfma": ("fdlp::ac_sweep_kernel", "fdlp::ac_band_kernel"),
+                              "direct": ("fdlp::autocorr_kernel",)},
+                 "lpc_env": ("fdlp::durbin8_kernel", "fdlp::lpc_env_lattice_kernel", "fdlp::cep_kernel",
+                             "fdlp::env_gemm_kernel"),
+                 "ola_log": ("fdlp::ola_log",)}
 
 
-def pmc_rows():
+def stage_kernel_prefixes(stage, path):
+    k = STAGE_KERNELS[stage]
+    return k[path] if isinstance(k, dict) else k
+
+
+def pmc_rows(pmc_file=None):
     try:
-        return {k.replace("void ", ""): m for k, m in json.load(open(PMC_FILE)).items()}
+        return {k.replace("void ", ""): m for k, m in json.load(open(pmc_file or PMC_FILE)).items()}
     except (OSError, ValueError, TypeError):
         return {}
 
 
-def stage_pmc(path):
-    """(HBM bytes per launch, bound) of the autocorrelation stage from the committed rocprofv3 PMC summary
-    of this same bench command (scripts/round_evidence.sh -> scripts/pmc_report.py).  Bytes: FETCH_SIZE x 2
-    (gfx950 correction, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.  Bound: the fp64 pipe that is busier,
-    time-weighted over the stage's kernels (SQ_ACTIVE_INST_VALU vs SQ_VALU_MFMA_BUSY_CYCLES)."""
-    tot, seen, valu, mfma = 0.0, set(), 0.0, 0.0
-    for name, m in pmc_rows().items():
-        for pre in AC_KERNEL_PREFIX[path]:
-            if name.startswith(pre) and "fetch_bytes_x2" in m and "write_bytes" in m:
-                tot += m["fetch_bytes_x2"] + m["write_bytes"]
-                seen.add(pre)
-                valu += m.get("valu_active_pct_per_simd", 0.0) * m.get("avg_ms", 0.0)
-                mfma += m.get("mfma_busy_pct", 0.0) * m.get("avg_ms", 0.0)
-    if len(seen) != len(AC_KERNEL_PREFIX[path]):
-        return None, "fp64-mfma" if path == "structured_mfma" or path == "direct" else "fp64-valu"
+def stage_pmc(prefixes, pmc_file=None):
+    """(HBM bytes per launch, bound) of a stage's kernels from the committed rocprofv3 PMC summary of the
+    same bench command (scripts/round_evidence.sh -> scripts/pmc_report.py).  Bytes: FETCH_SIZE x 2 (gfx950
+    correction, MI355X_MICROARCH.md "HBM") + WRITE_SIZE.  Bound: the fp64 pipe that is busier, time-weighted
+    over the stage's kernels (SQ_ACTIVE_INST_VALU vs SQ_VALU_MFMA_BUSY_CYCLES); (None, None) without data."""
+    tot, seen, valu, mfma = 0.0, 0, 0.0, 0.0
+    for name, m in pmc_rows(pmc_file).items():
+        if any(name.startswith(pre) for pre in prefixes) and "fetch_bytes_x2" in m and "write_bytes" in m:
+            tot += m["fetch_bytes_x2"] + m["write_bytes"]
+            seen += 1
+            valu += m.get("valu_active_pct_per_simd", 0.0) * m.get("avg_ms", 0.0)
+            mfma += m.get("mfma_busy_pct", 0.0) * m.get("avg_ms", 0.0)
+    if not seen:
+        return None, None
     return tot, ("fp64-valu" if valu >= mfma else "fp64-mfma")
 
 
-def step_pmc_bytes():
+def step_pmc_bytes(pmc_file=None):
     """HBM bytes of one batch: every fdlp kernel of the PMC summary, FETCH_SIZE x 2 + WRITE_SIZE per
     launch (one launch of each per batch, default pipeline)."""
-    rows = pmc_rows()
+    rows = pmc_rows(pmc_file)
     tot = [m["fetch_bytes_x2"] + m["write_bytes"] for k, m in rows.items()
            if k.startswith("fdlp::") and "fetch_bytes_x2" in m and "write_bytes" in m]
     return sum(tot) if tot else None
 
 
-AC_KERNELS = {"structured": "autocorr stage: ac_vsweep_kernel x2 (fp64 VALU FMA, lag-parallel sweeps) + "
-                            "ac_band_kernel (v_mfma_f64_16x16x4f64 straddles); the 78.6 TFLOP/s fp64 peak is "
-                            "shared by the VALU and matrix pipes",
-              "structured_mfma": "autocorr stage: ac_sweep_kernel + ac_band_kernel (v_mfma_f64_16x16x4f64)",
-              "direct": "autocorr stage: autocorr_kernel (v_mfma_f64_16x16x4f64)"}
+STAGE_DESC = {"dct": "DCT stage: frames_dft1 + dft2_dct (four-step Makhoul DCT-II, fp64 VALU)",
+              "autocorr": {"structured": "autocorr stage: ac_vsweep_kernel x2 (fp64 VALU FMA, lag-parallel sweeps) + "
+                                         "ac_band_kernel (v_mfma_f64_16x16x4f64 straddles); the 78.6 TFLOP/s fp64 "
+                                         "peak is shared by the VALU and matrix pipes",
+                           "structured_mfma": "autocorr stage: ac_sweep_kernel + ac_band_kernel (v_mfma_f64_16x16x4f64)",
+                           "direct": "autocorr stage: autocorr_kernel (v_mfma_f64_16x16x4f64)"},
+              "lpc_env": "LPC stage: durbin8_kernel (Levinson-Durbin) + cepstrum + envelope kernels (fp64)",
+              "ola_log": "OLA + log stage: ola_log_tiled_kernel"}
+
+
+def lpc_flops(p, M, Me, kk):
+    """Useful fp64 FLOPs of the LPC stage per (frame, band) item, 2 per MAC: the Durbin recursion (order k:
+    a k-term dot product and k - 1 updates, sum = p^2 MACs) and the off-by-one gain (p + 1), the LPC
+    cepstrum c_n, n < Me (features.py:233-246: min(n - 1, p) terms each; only the Me = min(M, env_nfft)
+    coefficients the envelope uses are computed), the envelope sum_n c'_n cos(2 pi n t / env_nfft) for
+    kk samples (Me x kk MACs) and its exp x window (2 per sample)."""
+    cep = sum(min(n - 1, p) for n in range(2, Me))
+    return 2.0 * (p * p + p + 1) + 2.0 * cep + 2.0 * Me * kk + 2.0 * kk
+
+
+def dct_flops(N):
+    """DCT-II of one frame as the FFT route counts it (2.5 N log2 N) plus the window (N)."""
+    return 2.5 * N * np.log2(N) + N
 
 
 def autocorr_flops(plan, support):
@@ -222,24 +350,36 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="wsj", choices=["wsj", "reverb"])
+    ap.add_argument("--config", default="wsj", choices=["wsj", "reverb", "chime4"])
     ap.add_argument("--utts", type=int, default=1024, help="utterances per step per GPU (wsj workload)")
     ap.add_argument("--seconds", type=float, default=4.0, help="utterance length (wsj workload)")
     ap.add_argument("--support-eps", type=float, default=None)
     ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1))
-    ap.add_argument("--cpu-per-worker", type=int, default=8)
+    ap.add_argument("--cpu-per-worker", type=int, default=None,
+                    help="utterances per CPU-baseline process (default: about 10 s of oracle time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-transfers", action="store_true", help="skip the PCIe-inclusive timed pass")
     ap.add_argument("--pipeline", type=int, default=None, help="sub-batches over two streams (plan default 1)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="device batches in flight per GPU: independent plans on their own HIP streams, each "
                          "featurising its own batch every step (their kernels overlap on the device)")
-    ap.add_argument("--workload", default="wsj", choices=["wsj", "librispeech"],
-                    help="wsj: --utts utterances of --seconds per GPU (BASELINE configs[1]); librispeech: U(1,30) s "
-                         "utterances, --frames analysis frames per GPU (configs[4])")
-    ap.add_argument("--frames", type=int, default=4096, help="analysis frames per step per GPU (librispeech)")
+    ap.add_argument("--workload", default=None, choices=["wsj", "librispeech", "reverb"],
+                    help="wsj: --utts utterances of --seconds per GPU (configs[1], [3]); librispeech: U(1,30) s "
+                         "(configs[4]); reverb: U(2,15) s reverberant sets (configs[2]); default from --config")
+    ap.add_argument("--frames", type=int, default=4096, help="analysis frames per step per GPU (U(a,b) workloads)")
     ap.add_argument("--dry-run", action="store_true", help="launcher + sharding + reduction only, no device work")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.workload is None:
+        a.workload = {"wsj": "wsj", "reverb": "reverb", "chime4": "wsj"}[a.config]
+    return a
+
+
+WORKLOAD_NAME = {("wsj", "wsj"): "wsj_si284_4s_batches", ("wsj", "librispeech"): "librispeech_960h_scale_u1_30s",
+                 ("reverb", "reverb"): "reverb_et_real_1ch_8ch_u2_15s", ("chime4", "wsj"): "chime4_tr05_4s_babble20db"}
+
+
+def workload_name(a):
+    return WORKLOAD_NAME.get((a.config, a.workload), "%s_params_%s_lengths" % (a.config, a.workload))
 
 
 def main():
@@ -251,19 +391,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print("bench.py: --gpus %d, WORLD_SIZE %d: running %d ranks" % (args.gpus, world, world), file=sys.stderr)
-
-    # CPU baseline first (fork before any GPU initialisation in this process), rank 0 at N=1 only
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
-        cpu = cpu_baseline(args.config, int(round(args.seconds * 16000)), args.cpu_workers, args.cpu_per_worker)
+    noise_host = babble_noise() if args.config == "chime4" else None
 
     import torch
     import torch.distributed as dist
-    from speech_recognition_tools_amd import FdlpPlan, FeatureConfig, PyRandom
+    from speech_recognition_tools_amd import FdlpPlan, FeatureConfig, NpRandom, PyRandom
     from speech_recognition_tools_amd.shard import shard_of, split_counts, timed_steps
-
-    if world > 1:  # host-side rendezvous: the only cross-rank traffic is a barrier and a max (no RCCL)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     cfg = getattr(FeatureConfig, args.config)()
     if args.support_eps is not None:
@@ -272,14 +405,20 @@ def main():
     full = scp_list(args.workload, world, args.utts, args.seconds, args.frames, lambda t: probe.geometry(t)[0])
     mine = shard_of(full, rank, world)
     first = sum(split_counts(len(full), world)[:rank])
-    lens = [t for _, t, _ in mine]
-    geo = [probe.geometry(t) for t in lens]
-    frames = sum(g[0] for g in geo)
-    rows_out = sum(g[1] for g in geo)
-    nj = sum(g[0] - 1 for g in geo)
-    audio_s = sum(lens) / 16000.0
+
+    # CPU baseline first (fork before any GPU initialisation in this process), rank 0 at N=1 only
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
+        per = args.cpu_per_worker or (10 if args.config == "reverb" else 24)
+        cpu = cpu_baseline(args.config, [t for _, t, _ in mine], args.cpu_workers, per, noise_host)
+
+    if world > 1:  # host-side rendezvous: the only cross-rank traffic is a barrier and a max (no RCCL)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     if args.dry_run:
+        lens = [t for _, t, _ in mine]
+        frames = sum(probe.geometry(t)[0] for t in lens)
+
         def step():
             pass
         sync = lambda: None
@@ -292,6 +431,7 @@ def main():
         if rank == 0:
             print(json.dumps({"metric": METRIC, "value": None, "unit": "audio-hours/s", "n_gpus": world,
                               "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+                              "config": {"workload": workload_name(args)},
                               "scp_entries": len(full), "shards": shards, "elapsed_s": elapsed}))
         if world > 1:
             dist.destroy_process_group()
@@ -301,13 +441,24 @@ def main():
     # N > 1 path on a small box, not a scaling measurement)
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
+    # input synthesis (untimed): speech-like int16 PCM; REVERB: reverberated on the device, back as int16
+    if args.workload == "reverb":
+        pcm_host, lens = reverb_pcm(mine, dev)
+    else:
+        pcm_host = utterance_pcm(mine)
+        lens = [t for _, t, _ in mine]
+    geo = [probe.geometry(t) for t in lens]
+    frames = sum(g[0] for g in geo)
+    rows_out = sum(g[1] for g in geo)
+    nj = sum(g[0] - 1 for g in geo)
+    audio_s = sum(lens) / 16000.0
+
     plan = FdlpPlan(cfg, device=dev.index, max_frames=frames)
     if args.pipeline is not None:
         plan.set_pipeline(args.pipeline)
     _, lo, hi = probe.fbank()
     support = (hi - lo).astype(np.int64)
 
-    pcm_host = utterance_pcm(mine)
     pcm = torch.from_numpy(pcm_host).to(dev)
     out = torch.empty((rows_out, cfg.nfilters), dtype=torch.float32, device=dev)
     rng = PyRandom(7 + rank)
@@ -315,23 +466,33 @@ def main():
     dd = dist if world > 1 else None
     cpu_dev = torch.device("cpu")
 
-    def step():
-        plan.compute(pcm, lens, rng.randbits2(nj), out=out)
-
     # B batches in flight: plan b (own workspace) featurises its own batch on its own stream every step;
     # the streams' kernels overlap on the device (the DCT and band kernels are latency-bound, the sweeps
     # VALU-bound).  Batch b holds the same utterance lengths with its own samples (the concatenated
     # signals rotated), and its own output buffer.
     B = max(1, args.inflight)
     plans = [plan] + [FdlpPlan(cfg, device=dev.index, max_frames=frames) for _ in range(B - 1)]
-    pcms = [pcm] + [torch.roll(pcm, 7919 * b) for b in range(1, B)]
+    shifts = [7919 * b for b in range(B)]
+    pcms = [pcm] + [torch.roll(pcm, shifts[b]) for b in range(1, B)]
     outs = [out] + [torch.empty_like(out) for _ in range(B - 1)]
     streams = [torch.cuda.Stream(dev) for _ in range(B)]
+    # CHiME4: --add_noise babble,20 mixed inside the timed kernels; the per-utterance (offset, alpha) are
+    # host-side descriptors of the batch (like its lengths), drawn once per batch in scp order
+    mix = [{} for _ in range(B)]
+    if noise_host is not None:
+        noise_dev = torch.from_numpy(noise_host).to(dev)
+        nr = NpRandom(31 + rank)
+        for b in range(B):
+            offs, alps = noise_mix(np.roll(pcm_host, shifts[b]), lens, noise_host, NOISE_SNR, nr)
+            mix[b] = dict(noise=noise_dev, noise_off=offs, noise_alpha=alps)
+
+    def step():
+        plan.compute(pcm, lens, rng.randbits2(nj), out=out, **mix[0])
 
     def step_inflight():
         for b in range(B):
             with torch.cuda.stream(streams[b]):
-                plans[b].compute(pcms[b], lens, rng.randbits2(nj), out=outs[b])
+                plans[b].compute(pcms[b], lens, rng.randbits2(nj), out=outs[b], **mix[b])
 
     # 1) headline: device-resident input and output, no profiling events.  warmup, barrier + sync,
     #    exactly K steps, sync + barrier, max over ranks (speech_recognition_tools_amd.shard)
@@ -376,7 +537,7 @@ def main():
             comp[b].wait_event(ev_in[b])
             comp[b].wait_event(ev_out[b])                # out_d[b] copied out by its previous D2H
             with torch.cuda.stream(comp[b]):
-                plans[b if B > 1 else 0].compute(pcm_d[b], lens, rng.randbits2(nj), out=out_d[b])
+                plans[b if B > 1 else 0].compute(pcm_d[b], lens, rng.randbits2(nj), out=out_d[b], **mix[b if B > 1 else 0])
                 ev_done[b].record(comp[b])
             s_out.wait_event(ev_done[b])
             with torch.cuda.stream(s_out):
@@ -402,15 +563,26 @@ def main():
     audio_h = world * args.steps * B * audio_s / 3600.0
     value = audio_h / elapsed
     ms_step = elapsed / args.steps * 1e3
-    # dominant stage: the autocorrelation (DESIGN.md "Roofline": useful MACs of the algorithm run)
-    flops_per_launch = autocorr_flops(plan, support) * frames
-    ac_ms = stages["autocorr"] / max(ncalls, 1)
-    achieved = flops_per_launch / (ac_ms * 1e-3) / 1e12
-    traffic, bound = stage_pmc(plan.autocorr_path)
+    # dominant stage of the one-batch profiled pass (fdlp_stage_times: HIP events on the kernels' stream);
+    # its algorithmic FLOPs are the useful work of the algorithm that stage runs (DESIGN.md "Measurement")
+    sms = {k: v / max(ncalls, 1) for k, v in stages.items()}
+    stage_ms = {"dct": sms["frames_dft1"] + sms["dft2_dct"], "autocorr": sms["autocorr"],
+                "lpc_env": sms["lpc_env"], "ola_log": sms["ola_log"]}
+    dom = max(stage_ms, key=stage_ms.get)
+    items = frames * plan.B
+    Me = min(cfg.coeff_num, 2 * plan.kk)
+    stage_flops = {"dct": dct_flops(plan.N) * frames, "autocorr": autocorr_flops(plan, support) * frames,
+                   "lpc_env": lpc_flops(cfg.order, cfg.coeff_num, Me, plan.kk) * items,
+                   "ola_log": 2.0 * items * plan.kk}
+    pmc_file = _latest_pmc(args.config if args.workload != "librispeech" else "librispeech") or PMC_FILE
+    path = plan.autocorr_path
+    traffic, bound = stage_pmc(stage_kernel_prefixes(dom, path), pmc_file)
+    dom_ms = stage_ms[dom]
+    achieved = stage_flops[dom] / (dom_ms * 1e-3) / 1e12
     ac_can, whole_can = canonical_flops(plan.N, plan.B, cfg.order, cfg.coeff_num, plan.kk, 2 * plan.kk)
     # algorithmic HBM bytes (north_star / SURVEY 8(d)): int16 PCM in + float32 features out
     alg_bytes = float(B * (pcm_host.nbytes + out.numel() * 4))
-    pmc_step = step_pmc_bytes()
+    pmc_step = step_pmc_bytes(pmc_file)
     pmc_step = B * pmc_step if pmc_step else pmc_step  # B batches per step
     hbm = {"algorithmic_bytes_per_step": alg_bytes,
            "algorithmic_GBps": alg_bytes / (ms_step * 1e-3) / 1e9,
@@ -420,8 +592,9 @@ def main():
            "counter_frac": pmc_step / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS if pmc_step else None,
            "peak_GBps": HBM_PEAK_GBS,
            "counter_source": "FETCH_SIZE x 2 + WRITE_SIZE summed over every kernel of one step, rocprofv3 PMC "
-                             "passes of this command, %s" % os.path.relpath(PMC_FILE or "none", ROOT),
+                             "passes of this command, %s" % os.path.relpath(pmc_file or "none", ROOT),
            "note": "the path is fp64-compute-bound; HBM does not bound it (SURVEY.md 8(d))"}
+    desc = STAGE_DESC[dom]
     res = {
         "metric": METRIC,
         "value": value,
@@ -435,24 +608,31 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": ("librispeech_960h_scale_u1_30s" if args.workload == "librispeech" else
-                                "wsj_si284_4s_batches" if args.config == "wsj" else "reverb_et_4s_batches"),
+        "config": {"workload": workload_name(args),
+                   "params": args.config,
                    "scp_entries_total": len(full),
                    "utts_per_step_per_gpu": B * len(lens),
                    "batches_in_flight": B,
                    "utts_per_batch": len(lens),
-                   "utt_seconds": args.seconds if args.workload == "wsj" else "U(1,30), mean %.2f" % (
-                       audio_s / max(len(lens), 1)),
+                   "utt_seconds": args.seconds if args.workload == "wsj" else "%s, mean %.2f" % (
+                       "U(1,30)" if args.workload == "librispeech" else "U(2,15)", audio_s / max(len(lens), 1)),
                    "frames_per_step_per_gpu": B * frames, "nfilters": cfg.nfilters, "order": cfg.order,
-                   "coeff_num": cfg.coeff_num, "fbank": cfg.fbank_type, "support_eps": cfg.support_eps,
-                   "autocorr_path": plan.autocorr_path,
+                   "coeff_num": cfg.coeff_num, "coeff_range": cfg.coeff_range, "fbank": cfg.fbank_type,
+                   "support_eps": cfg.support_eps, "autocorr_path": path,
+                   "add_noise": "babble,%g (on the device, in the timed kernels)" % NOISE_SNR
+                   if noise_host is not None else "clean",
+                   "reverb_sets": ("1ch T60 0.7 s / 8ch_beamformit T60 0.35 s, synthetic RIRs applied by "
+                                   "fdlp_reverb before timing" if args.workload == "reverb" else None),
                    "parallelism": "scp-shard x%d (contiguous split_scp shards, no collective)" % world},
-        "roofline": {"bound": bound, "kernel": AC_KERNELS[plan.autocorr_path],
+        "roofline": {"bound": bound or "fp64-valu", "stage": dom,
+                     "kernel": desc[path] if isinstance(desc, dict) else desc,
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "traffic_unit": "bytes/launch (rocprofv3 PMC, %s)" % os.path.relpath(PMC_FILE or "none", ROOT),
-                     "avg_launch_ms": ac_ms, "algorithmic_flops_per_launch": flops_per_launch,
-                     "canonical_frac": ac_can * frames / (ac_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                     "traffic_unit": "bytes/launch (rocprofv3 PMC, %s)" % os.path.relpath(pmc_file or "none", ROOT),
+                     "avg_launch_ms": dom_ms, "algorithmic_flops_per_launch": stage_flops[dom],
+                     "stage_fracs": {k: stage_flops[k] / (stage_ms[k] * 1e-3) / 1e12 / FP64_PEAK_TFLOPS
+                                     for k in stage_ms if stage_ms[k] > 0},
+                     "canonical_frac": ac_can * frames / (sms["autocorr"] * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
                      "canonical_frac_whole_step": whole_can * B * frames / (ms_step * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
                      "canonical_note": "canonical = SURVEY.md 8(d) FFT-route FLOPs (%.1f MFLOP/frame autocorr, %.1f "
                                        "whole path); the exact structured algorithm runs ~5x fewer FLOPs than the FFT "
@@ -460,7 +640,7 @@ def main():
                                        "measure; frac uses the FLOPs the path actually runs" %
                                        (ac_can / 1e6, whole_can / 1e6)},
         "hbm": hbm,
-        "stage_ms_per_step": {k: v / max(ncalls, 1) for k, v in stages.items()},
+        "stage_ms_per_step": sms,
         "ms_per_batch_profiled": elapsed_prof / args.steps * 1e3,
         "one_batch_in_flight": {"value": world * args.steps * audio_s / 3600.0 / elapsed_one,
                                 "ms_per_step": elapsed_one / args.steps * 1e3,

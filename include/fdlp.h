@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define FDLP_ABI_VERSION 3
+#define FDLP_ABI_VERSION 4
 
 enum {
   FDLP_OK = 0,
@@ -282,7 +282,8 @@ int fdlp_wav_parse(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* cha
                    const int16_t** samples, int64_t* n_samples);
 /* Any RIFF/RIFX WAVE buffer scipy.io.wavfile.read accepts (PCM 1-64 bit, <= 8 bit unsigned, 3/5/6/7-byte
  * containers left-justified; IEEE float 32/64; WAVE_FORMAT_EXTENSIBLE): sample rate, channels, frames, and
- * *is_int16 = 1 when scipy would return int16.  With out != NULL the interleaved samples are written as
+ * *is_int16 = 1 when scipy would return little-endian int16 (the samples can be used in place, fdlp_wav_parse),
+ * 2 for big-endian (RIFX) int16 (decode; the values are int16), 0 otherwise.  With out != NULL the interleaved samples are written as
  * the double values of scipy's array (ABI 3). */
 int fdlp_wav_decode(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* channels, int32_t* is_int16,
                     int64_t* n_samples, double* out);
@@ -293,6 +294,9 @@ int fdlp_ark_open(const char* ark_path, const char* scp_path, fdlp_ark_writer** 
 int fdlp_ark_write(fdlp_ark_writer* w, const char* utt, const float* mat, int32_t rows,
                    int32_t cols);
 int fdlp_ark_close(fdlp_ark_writer* w);
+/* Closes the writer and deletes <path>.tmp without publishing: the failure path of a JOB, so its outputs
+ * appear complete or not at all (ABI 4). */
+int fdlp_ark_abort(fdlp_ark_writer* w);
 /* Kaldi matrix reader for `compute-cmvn-stats`-style rspecifiers: "scp:<feats.scp>" (lines
  * "<utt> <ark path>:<offset>") or "ark:<file>" (binary ark, "-" = stdin).  Float ("FM") and double
  * ("DM") binary matrices; data is returned as float32 (double matrices are narrowed, as Kaldi's

@@ -3,7 +3,11 @@
 # sadhusamik/speech_recognition_tools (same options and outputs), running each JOB's
 # compute-fdlp-feats on an MI355X.  Extra options: --ngpu N (JOB n runs on GPU (n-1) mod N, with or
 # without a Kaldi $cmd launcher: the CLI gets --device_rr=JOB,N and picks the device before any GPU
-# call), --jobs_per_gpu K (without $cmd: at most N*K JOBs run at once; default 2).
+# call, folded into the GPUs that JOB can see; default: every visible GPU, counted without touching
+# HIP -- HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES if set, else the KFD
+# topology's GPU nodes -- so a recipe that calls the driver unchanged, e.g. --cmd "$train_cmd" --nj 20
+# (e2e/wsj/run_fdlp_e1.sh:196), spreads its JOBs over the node), --jobs_per_gpu K (without $cmd: at most
+# N*K JOBs run at once; default 2).
 #
 #   make_FDLPspectrum_feats.sh [--opts] <data_dir> <feat_dir>
 # Inputs: <data_dir>/wav.scp or <data_dir>/segments.  Outputs: <data_dir>/feats.scp,
@@ -31,7 +35,7 @@ spectrum_type=log
 write_utt2num_frames=false
 lifter_config=
 check_for_segment="data/train"
-ngpu=1
+ngpu=          # default: the visible GPU count (visible_gpus below)
 jobs_per_gpu=2  # two JOBs per GPU overlap each other's latency-bound kernels
 compute_cmvn=false   # also write <data_dir>/cmvn.ark (global CMVN stats, fused on the device)
 seed=
@@ -50,6 +54,23 @@ else
     eval "$k=\"\$v\""
   done
 fi
+
+visible_gpus() {  # GPUs this process may use, without initialising HIP
+  local v n=0 f id
+  for v in HIP_VISIBLE_DEVICES ROCR_VISIBLE_DEVICES CUDA_VISIBLE_DEVICES; do
+    if [ -n "${!v+x}" ]; then
+      IFS=, read -ra ids <<< "${!v}"
+      for id in "${ids[@]}"; do [ -n "${id// /}" ] && n=$((n + 1)); done
+      echo $n; return
+    fi
+  done
+  for f in /sys/class/kfd/kfd/topology/nodes/*/gpu_id; do
+    [ -r "$f" ] && read -r id < "$f" && [ "${id:-0}" != 0 ] && n=$((n + 1))
+  done
+  echo $n
+}
+[ -z "$ngpu" ] && ngpu=$(visible_gpus)
+[ "${ngpu:-0}" -ge 1 ] 2>/dev/null || ngpu=1
 
 here="$(cd "$(dirname "${BASH_SOURCE[0]}")/.." && pwd)"
 [ -z "$src_dir" ] && src_dir="$here/speech_recognition_tools_amd"

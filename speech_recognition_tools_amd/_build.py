@@ -37,10 +37,10 @@ def build(force=False, verbose=False, out=None, defines=()):
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     os.makedirs(os.path.dirname(os.path.abspath(target)), exist_ok=True)
-    objs = []
+    objs, procs = [], []
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function",
              "-munsafe-fp-atomics"] + list(defines)
-    for src in SOURCES:
+    for src in SOURCES:  # the four translation units compile in parallel
         obj = os.path.join(LIBDIR, src + ".ab.o" if out else src + ".o")
         lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "c++"]
         cmd = [hipcc()] + flags + lang + ["-c", os.path.join(CSRC, src), "-o", obj]
@@ -49,8 +49,11 @@ def build(force=False, verbose=False, out=None, defines=()):
                    "-x", "c++", "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
+        procs.append((subprocess.Popen(cmd), cmd))
         objs.append(obj)
+    failed = [cmd for p, cmd in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
     tmp = target + ".tmp"
     cmd = [hipcc(), "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", tmp] + objs
     subprocess.run(cmd, check=True)

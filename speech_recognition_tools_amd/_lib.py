@@ -143,6 +143,7 @@ SIGNATURES = {
     "fdlp_ark_open": (c_i32, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(c_p)]),
     "fdlp_ark_write": (c_i32, [c_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), c_i32, c_i32]),
     "fdlp_ark_close": (c_i32, [c_p]),
+    "fdlp_ark_abort": (c_i32, [c_p]),
     "fdlp_cmvn_accumulate": (c_i32, [c_p, c_i64, c_i32, c_p, c_p]),
     "fdlp_reverb": (c_i32, [ctypes.POINTER(FdlpReverbBatchC), c_p]),
     "fdlp_mel_plan_create": (c_i32, [ctypes.POINTER(FdlpMelConfigC), c_i32, ctypes.POINTER(c_p)]),
@@ -172,7 +173,7 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.fdlp_abi_version() != 3:
+    if lib.fdlp_abi_version() != 4:
         raise ImportError("libfdlp_hip.so ABI mismatch")
     return lib
 

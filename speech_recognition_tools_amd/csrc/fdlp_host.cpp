@@ -276,7 +276,9 @@ int fdlp_wav_decode(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* ch
   if (rc != FDLP_OK) return rc;
   if (srate) *srate = w.sr;
   if (channels) *channels = w.ch;
-  if (is_int16) *is_int16 = (w.fmt == 1 && w.bits > 8 && w.bps == 2 && !w.big) ? 1 : 0;
+  // 16-bit PCM is what scipy returns as int16 (RIFF '<i2' or RIFX '>i2'): 1 = little-endian (the samples
+  // can be used in place, fdlp_wav_parse), 2 = big-endian (decode, then the values are int16)
+  if (is_int16) *is_int16 = (w.fmt == 1 && w.bits > 8 && w.bps == 2) ? (w.big ? 2 : 1) : 0;
   if (n_samples) *n_samples = w.frames;
   if (out) {
     const int64_t n = w.frames * w.ch;
@@ -440,6 +442,18 @@ int fdlp_ark_close(fdlp_ark_writer* w) {
   }
   delete w;
   return rc;
+}
+
+// Closes the files and removes the temporaries: a JOB that fails part-way publishes nothing under the
+// final names (the reference raises before dict2Ark, so it never writes an ark either).
+int fdlp_ark_abort(fdlp_ark_writer* w) {
+  if (!w) return FDLP_OK;
+  if (w->ark) fclose(w->ark);
+  if (w->scp) fclose(w->scp);
+  remove(w->ark_tmp.c_str());
+  if (w->scp) remove(w->scp_tmp.c_str());
+  delete w;
+  return FDLP_OK;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -218,7 +218,16 @@ void read_entry(const std::string& line, Utt& u) {
   u.ch = ch;
   u.T = n;
   u.is_int16 = i16 != 0;
-  if (u.is_int16) {  // the samples stay in the file bytes (no copy until the batch buffer)
+  if (i16 == 2) {  // big-endian (RIFX) 16-bit PCM: scipy returns '>i2', so it is int16 input; swapped copy
+    auto swapped = std::make_shared<std::vector<uint8_t>>((size_t)n * ch * 2);
+    std::vector<double> v((size_t)n * ch);
+    if (fdlp_wav_decode(bytes->data(), (int64_t)bytes->size(), nullptr, nullptr, nullptr, nullptr, v.data()) != FDLP_OK)
+      return;
+    int16_t* d = (int16_t*)swapped->data();
+    for (size_t q = 0; q < v.size(); ++q) d[q] = (int16_t)v[q];
+    u.s16 = d;
+    u.raw = std::move(swapped);
+  } else if (u.is_int16) {  // the samples stay in the file bytes (no copy until the batch buffer)
     int32_t s2, c2;
     int64_t n2;
     const int16_t* smp = nullptr;
@@ -522,9 +531,11 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     if (s_out) (void)hipStreamDestroy(s_out);
     if (jrng) fdlp_pyrandom_destroy(jrng);
     if (nrng) fdlp_nprandom_destroy(nrng);
-    if (ark) {
+    if (ark && code != FDLP_OK) {
+      fdlp_ark_abort(ark);  // a failed JOB publishes no partial ark/scp
+    } else if (ark) {
       const int rc2 = fdlp_ark_close(ark);
-      if (code == FDLP_OK && rc2 != FDLP_OK) {
+      if (rc2 != FDLP_OK) {
         code = rc2;
         keep = fdlp::last_error_slot();
       }

@@ -2027,6 +2027,10 @@ __device__ __forceinline__ void cep_window(double& a0, double& a1, double& a2, d
     } else {
       lgkm_wait<0>();
     }
+    // the asm loads' results look ready to the compiler: tie them to the wait (a volatile asm that
+    // "rewrites" them), so neither the FMAs nor a register copy can be scheduled above it
+#pragma unroll
+    for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(va[q]));
     cep_fma16(a0, a1, a2, a3, kc[WI], va);
     cep_window<W, WI + 1>(a0, a1, a2, a3, kc, vb, va, addr);
   }

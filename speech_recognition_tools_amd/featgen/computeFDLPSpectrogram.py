@@ -75,14 +75,17 @@ def build_parser():
 
 
 def resolve_device(args):
-    """--device, else --device_rr "JOB,N" -> (JOB-1) mod N, else LOCAL_RANK, else 0."""
+    """--device, else --device_rr "JOB,N" -> (JOB-1) mod N, folded into the GPUs this process can see
+    (a scheduler that gives each JOB its own GPU leaves it one: device 0), else LOCAL_RANK, else 0."""
     if args.device is not None:
         return int(args.device)
     if getattr(args, 'device_rr', None):
+        from speech_recognition_tools_amd.shard import visible_gpu_count
         job, n = (int(v) for v in args.device_rr.split(','))
         if job < 1 or n < 1:
             raise ValueError('--device_rr needs JOB >= 1 and N >= 1')
-        return (job - 1) % n
+        vis = visible_gpu_count()
+        return (job - 1) % n % vis if vis > 0 else (job - 1) % n
     return int(os.environ.get("LOCAL_RANK", "0"))
 
 
@@ -240,6 +243,9 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
         flush()
         while inflight:
             complete(inflight.popleft())
+    except BaseException:  # a failed JOB publishes no partial ark/scp (fdlp_ark_abort)
+        ark.abort()
+        raise
     finally:
         ark.close()
     if args.write_utt2num_frames:                                           # :232-237

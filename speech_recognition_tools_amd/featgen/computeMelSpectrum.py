@@ -131,6 +131,9 @@ def compute_mel_spectrum(args, srate=16000, window=np.hamming, return_feats=Fals
             pending.append((uttid, sig, off, alpha))
             pending_frames += F
         flush()
+    except BaseException:  # a failed JOB publishes no partial ark/scp (fdlp_ark_abort)
+        ark.abort()
+        raise
     finally:
         ark.close()
     if args.write_utt2num_frames:                                            # :165-170

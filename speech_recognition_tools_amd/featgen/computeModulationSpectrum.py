@@ -137,6 +137,9 @@ def get_feats(args, srate=16000, return_feats=False):
             pending.append((uttid, sig))
             pending_frames += F
         flush()
+    except BaseException:  # a failed JOB publishes no partial ark/scp (fdlp_ark_abort)
+        ark.abort()
+        raise
     finally:
         ark.close()
     return feats_out

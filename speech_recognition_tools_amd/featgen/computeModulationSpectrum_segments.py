@@ -159,6 +159,9 @@ def get_feats(args, srate=16000, return_feats=False):
             pending.append((seg_id, signal))
             pending_frames += F
         flush()
+    except BaseException:  # a failed JOB publishes no partial ark/scp (fdlp_ark_abort)
+        ark.abort()
+        raise
     finally:
         ark.close()
     return feats_out

@@ -28,7 +28,12 @@ def read_wav_bytes(data: bytes):
     sr, ch, i16, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
     check(lib.fdlp_wav_decode(ptr(buf, ctypes.c_uint8), buf.size, ctypes.byref(sr), ctypes.byref(ch),
                               ctypes.byref(i16), ctypes.byref(n), None))
-    if i16.value:
+    if i16.value == 2:  # big-endian (RIFX) 16-bit PCM: scipy returns '>i2' values, i.e. int16 input
+        x = np.empty(n.value * ch.value, dtype=np.float64)
+        check(lib.fdlp_wav_decode(ptr(buf, ctypes.c_uint8), buf.size, None, None, None, None,
+                                  ptr(x, ctypes.c_double)))
+        x = x.astype(np.int16)
+    elif i16.value:
         sp = ctypes.POINTER(ctypes.c_int16)()
         sr2, ch2, n2 = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
         check(lib.fdlp_wav_parse(ptr(buf, ctypes.c_uint8), buf.size, ctypes.byref(sr2), ctypes.byref(ch2),
@@ -139,8 +144,10 @@ def dict2Ark(feat_dict, outfile, kaldi_cmd=None):
             if m.ndim != 2:
                 raise ValueError("feature matrix must be 2-D")
             check(lib.fdlp_ark_write(h, key.encode(), ptr(m, ctypes.c_float), m.shape[0], m.shape[1]))
-    finally:
-        check(lib.fdlp_ark_close(h))
+    except BaseException:  # nothing is published under the final names (fdlp_ark_abort)
+        lib.fdlp_ark_abort(h)
+        raise
+    check(lib.fdlp_ark_close(h))
 
 
 def read_ark(path):

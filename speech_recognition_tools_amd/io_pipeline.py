@@ -108,12 +108,22 @@ class ArkStream:
             check(lib.fdlp_ark_write(self._h, key.encode(), ptr(m, ctypes.c_float), m.shape[0], m.shape[1]))
 
     def close(self):
+        """Publish: rename the .tmp files to their final names."""
         if self._h:
             h, self._h = self._h, ctypes.c_void_p()
             check(lib.fdlp_ark_close(h))
 
+    def abort(self):
+        """Failure path: delete the .tmp files, publish nothing (fdlp_ark_abort)."""
+        if self._h:
+            h, self._h = self._h, ctypes.c_void_p()
+            lib.fdlp_ark_abort(h)
+
+    def finish(self, ok: bool):
+        self.close() if ok else self.abort()
+
     def __enter__(self):
         return self
 
-    def __exit__(self, *exc):
-        self.close()
+    def __exit__(self, exc_type, *exc):
+        self.finish(exc_type is None)

@@ -5,7 +5,27 @@ collective on the data path; the only cross-rank traffic is the bench's barrier 
 
 No torch / library import at module level: the driver script calls split_lists() from a plain python3.
 """
+import glob
+import os
 import time
+
+
+def visible_gpu_count():
+    """GPUs this process may use, without initialising HIP: the first of HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES that is set (its entry count), else the KFD topology's
+    GPU nodes (gpu_id != 0).  The same rule as scripts/make_FDLPspectrum_feats.sh's visible_gpus."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip()])
+    n = 0
+    for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id"):
+        try:
+            with open(f) as fh:
+                n += int(fh.read().strip() or 0) != 0
+        except (OSError, ValueError):
+            pass
+    return n
 
 
 def split_counts(n, k):

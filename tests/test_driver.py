@@ -17,6 +17,7 @@ def _resolve(argv):
 
 def test_resolve_device_options(monkeypatch):
     monkeypatch.delenv("LOCAL_RANK", raising=False)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
     assert _resolve(["a.scp", "o"]) == 0
     assert _resolve(["a.scp", "o", "--device_rr=7,4"]) == 2
     assert _resolve(["a.scp", "o", "--device_rr=7,4", "--device=1"]) == 1
@@ -24,22 +25,45 @@ def test_resolve_device_options(monkeypatch):
     assert _resolve(["a.scp", "o"]) == 3
     with pytest.raises(ValueError):
         _resolve(["a.scp", "o", "--device_rr=0,4"])
+    # a scheduler that hands each JOB its own GPU: the round-robin index folds into what the JOB sees
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "5")
+    assert _resolve(["a.scp", "o", "--device_rr=7,4"]) == 0
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "2,3")
+    assert _resolve(["a.scp", "o", "--device_rr=7,4"]) == 0
+    assert _resolve(["a.scp", "o", "--device_rr=4,4"]) == 1
 
 
-@pytest.mark.parametrize("nj,ngpu", [(5, 2), (4, 8)])
-def test_driver_cmd_branch_spreads_jobs_over_gpus(tmp_path, nj, ngpu):
+def test_visible_gpu_count(monkeypatch):
+    from speech_recognition_tools_amd.shard import visible_gpu_count
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1,2")
+    assert visible_gpu_count() == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")  # HIP's list wins (it indexes into ROCR's)
+    assert visible_gpu_count() == 1
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert visible_gpu_count() == 0
+
+
+@pytest.mark.parametrize("nj,ngpu", [(5, 2), (4, 8), (20, None)])
+def test_driver_cmd_branch_spreads_jobs_over_gpus(tmp_path, monkeypatch, nj, ngpu):
+    """ngpu None: the recipe's unchanged call (--cmd "$train_cmd" --nj 20, e2e/wsj/run_fdlp_e1.sh:196) on
+    an 8-GPU node: the driver counts the visible GPUs itself and spreads the JOBs over all of them."""
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
     data = tmp_path / "data" / "dev"
     data.mkdir(parents=True)
     (data / "wav.scp").write_text("".join("u%d /x/u%d.wav\n" % (i, i) for i in range(nj * 2)))
     log = tmp_path / "cmd.log"
     env = dict(os.environ, FAKE_CMD_LOG=str(log))
-    cmd = ["bash", os.path.join(ROOT, "scripts", "make_FDLPspectrum_feats.sh"), "--nj", str(nj), "--ngpu", str(ngpu),
+    gpu_opt = ["--ngpu", str(ngpu)] if ngpu else []
+    cmd = ["bash", os.path.join(ROOT, "scripts", "make_FDLPspectrum_feats.sh"), "--nj", str(nj)] + gpu_opt + [
            "--cmd", os.path.join(ROOT, "tests", "fakes", "fake_run_pl.sh"), "--write_utt2num_frames", "true",
            str(data), str(tmp_path / "fbank")]
     r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     lines = log.read_text().splitlines()
     assert len(lines) == nj
+    ngpu = ngpu or 8
     devices = []
     for n, line in enumerate(lines, 1):
         argv = line.split()[2:]  # drop "python3 <cli>"

@@ -119,6 +119,22 @@ def test_cli_rejects_other_sample_rates(tmp_path, runner):
         _run([scp, str(tmp_path / "o")], runner)
 
 
+@RUNNERS
+def test_cli_failure_leaves_no_partial_outputs(tmp_path, runner):
+    """An scp whose second entry is 8 kHz fails the JOB after the first utterance was featurised: the
+    reference raises before dict2Ark and writes nothing, so no .ark / .scp may appear (not even the
+    first utterance's), and no .tmp is left behind."""
+    a, b = str(tmp_path / "a.wav"), str(tmp_path / "b.wav")
+    wavfile.write(a, 16000, (np.random.default_rng(0).standard_normal(40000) * 1000).astype(np.int16))
+    wavfile.write(b, 8000, np.zeros(16000, dtype=np.int16))
+    scp = str(tmp_path / "w.scp")
+    open(scp, "w").write("u1 %s\nu2 %s\n" % (a, b))
+    with pytest.raises(AssertionError, match="different sampling rate"):
+        _run([scp, str(tmp_path / "o"), "--write_utt2num_frames"], runner)
+    left = sorted(f for f in os.listdir(str(tmp_path)) if f.startswith("o"))
+    assert left == [], left
+
+
 def _write_formats(tmp, x):
     """The int16 signal x in the WAV formats scipy reads, and the values scipy returns for each."""
     import struct

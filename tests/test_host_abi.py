@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     for name in syms:
         assert hasattr(_lib.lib, name), name
     assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
-    assert _lib.lib.fdlp_abi_version() == 3
+    assert _lib.lib.fdlp_abi_version() == 4
 
 
 @pytest.mark.parametrize("seed", [0, 1, 7, 1234, 2 ** 40 + 5, 2 ** 64 + 3])
@@ -236,6 +236,17 @@ def test_wav_decoder_matches_scipy_formats(tmp_path):
             sr2, want = read(p)
             assert want.dtype.kind == "i" and want.dtype.itemsize == 4
             np.testing.assert_array_equal(got, want.astype(np.float64))
+    # big-endian 16-bit PCM: scipy returns '>i2', i.e. int16 input (noise mixing / diff apply to it)
+    fmt = struct.pack(">HHIIHH", 1, 1, 16000, 32000, 2, 16)
+    raw = x.astype(">i2").tobytes()
+    body = b"WAVE" + b"fmt " + struct.pack(">I", len(fmt)) + fmt + b"data" + struct.pack(">I", len(raw)) + raw
+    blob = b"RIFX" + struct.pack(">I", len(body)) + body
+    p = str(tmp_path / "i16_be.wav")
+    open(p, "wb").write(blob)
+    sr, got = read_wav_bytes(blob)
+    sr2, want = read(p)
+    assert want.dtype.kind == "i" and want.dtype.itemsize == 2 and got.dtype == np.int16
+    np.testing.assert_array_equal(got, want)
 
 
 def test_wav_parser_rejects_garbage():
@@ -280,6 +291,25 @@ def test_ark_writer_is_atomic(tmp_path):
     assert sorted(os.listdir(str(tmp_path))) == ["j.1.ark", "j.1.scp"]
     line = open(out + ".scp").read().split()
     assert line[1].rsplit(":", 1)[0] == os.path.realpath(out + ".ark")
+
+
+def test_ark_writer_abort_publishes_nothing(tmp_path):
+    """fdlp_ark_abort (a JOB's failure path) deletes the temporaries: no ark/scp under any name."""
+    import ctypes
+    from speech_recognition_tools_amd._lib import check, lib
+    from speech_recognition_tools_amd.io_pipeline import ArkStream
+    h = ctypes.c_void_p()
+    out = str(tmp_path / "j.1")
+    check(lib.fdlp_ark_open((out + ".ark").encode(), (out + ".scp").encode(), ctypes.byref(h)))
+    m = np.ones((2, 3), dtype=np.float32)
+    check(lib.fdlp_ark_write(h, b"u", m.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), 2, 3))
+    check(lib.fdlp_ark_abort(h))
+    assert os.listdir(str(tmp_path)) == []
+    with pytest.raises(RuntimeError):
+        with ArkStream(out) as ark:
+            ark.write("u", m)
+            raise RuntimeError("JOB failed")
+    assert os.listdir(str(tmp_path)) == []
 
 
 def test_cli_argparse_surface_matches_reference():
