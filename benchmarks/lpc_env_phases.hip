@@ -3,7 +3,7 @@
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DFDLP_LPC_PHASES=7 -I speech_recognition_tools_amd/csrc \
 //         benchmarks/lpc_env_phases.hip -o benchmarks/lpc_env_p7
 // (mask bits: 1 Durbin, 2 cepstrum, 4 envelope).  r is the autocorrelation of an AR(2) process.
-#include "../speech_recognition_tools_amd/csrc/fdlp_kernels.hip"
+#include "../speech_recognition_tools_amd/csrc/fdlp_lpc.hip"
 
 #include <math.h>
 #include <stdio.h>

@@ -157,6 +157,14 @@ int fdlp_set_debug(fdlp_plan* plan, int32_t keep_intermediates);
 #define FDLP_AC_STRUCTURED_MFMA 3
 int fdlp_set_autocorr_path(fdlp_plan* plan, int32_t path);
 int fdlp_autocorr_path(const fdlp_plan* plan);
+/* LPC stage (Levinson-Durbin + cepstrum + envelope).  FDLP_LPC_AUTO (plan default): the register-resident
+ * lattice kernels (durbin8_kernel for 128 <= p <= 183, then the cepstrum / envelope kernel); FDLP_LPC_LDS:
+ * the LDS Durbin kernel for every p (the fallback for p > 255 and an independent cross-check; its
+ * order-k dot products are summed in another order).  The only switches between kernel variants are
+ * these explicit calls: nothing is read from the environment (ABI 4). */
+#define FDLP_LPC_AUTO 0
+#define FDLP_LPC_LDS 1
+int fdlp_set_lpc_path(fdlp_plan* plan, int32_t path);
 /* Lower-skirt / flat-top / upper-skirt split of every band, [0,m1) [m1,m2) [m2,N), used by the
  * STRUCTURED path; FDLP_E_INVALID when the filterbank does not have it. */
 int fdlp_plan_regions(const fdlp_plan* plan, int32_t* m1, int32_t* m2);

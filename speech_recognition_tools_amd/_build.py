@@ -7,8 +7,9 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libfdlp_hip.so")
-SOURCES = ["fdlp_kernels.hip", "fdlp_plan.cpp", "fdlp_host.cpp", "fdlp_job.cpp"]
-HEADERS = ["fdlp_internal.h", "fdlp_error.h", os.path.join("..", "..", "include", "fdlp.h")]
+SOURCES = ["fdlp_dct.hip", "fdlp_autocorr.hip", "fdlp_lpc.hip", "fdlp_misc.hip", "fdlp_plan.cpp", "fdlp_host.cpp",
+           "fdlp_job.cpp"]
+HEADERS = ["fdlp_internal.h", "fdlp_device.h", "fdlp_error.h", os.path.join("..", "..", "include", "fdlp.h")]
 ARCH = os.environ.get("FDLP_OFFLOAD_ARCH", "gfx950")
 
 
@@ -40,7 +41,7 @@ def build(force=False, verbose=False, out=None, defines=()):
     objs, procs = [], []
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function",
              "-munsafe-fp-atomics"] + list(defines)
-    for src in SOURCES:  # the four translation units compile in parallel
+    for src in SOURCES:  # the translation units compile in parallel
         obj = os.path.join(LIBDIR, src + ".ab.o" if out else src + ".o")
         lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "c++"]
         cmd = [hipcc()] + flags + lang + ["-c", os.path.join(CSRC, src), "-o", obj]

@@ -124,6 +124,7 @@ SIGNATURES = {
     "fdlp_autocorr_path": (c_i32, [c_p]),
     "fdlp_plan_regions": (c_i32, [c_p, c_p, c_p]),
     "fdlp_plan_flat_events": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_i32]),
+    "fdlp_set_lpc_path": (c_i32, [c_p, c_i32]),
     "fdlp_set_pipeline": (c_i32, [c_p, c_i32]),
     "fdlp_stage_times": (c_i32, [c_p, P_dbl, P_i32]),
     "fdlp_dct_rows": (c_i32, [c_p, c_p, c_i32, c_p, c_p]),

@@ -1,0 +1,529 @@
+// fdlp_dct.hip -- gfx950 kernels of the DCT stage:
+//   1. frames_dft1 : int16/f64 PCM -> reflect pad -> window -> Makhoul reorder -> column DFTs (length N1)
+//                    of the four-step N = N1*N2 DFT, twiddled (getFrames features.py:118-154, :174-178)
+//   2. dft2_dct    : row DFTs (length N2) -> Makhoul post-twiddle -> DCT-II/sqrt(2N) (:178)
+// fp64 throughout.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include <algorithm>
+#include <type_traits>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "fdlp_device.h"
+
+namespace fdlp {
+
+// -----------------------------------------------------------------------------------------
+// 1. frames -> Makhoul-reordered real sequence -> column DFTs (length N1) + four-step twiddle
+// -----------------------------------------------------------------------------------------
+// Windowed frame sample at Makhoul index n of v (v[n] = x[2n], v[N-1-n] = x[2n+1]).
+__device__ __forceinline__ double makhoul_sample(const DevConsts& c, const FrameDesc& fd, int n, int f,
+                                                 const void* __restrict__ pcm, int pcm_kind,
+                                                 const int16_t* __restrict__ noise,
+                                                 const double* __restrict__ dense_rows) {
+  const int N = c.N;
+  // Makhoul even/odd split; complex modulation: sample order (scipy.fftpack.ifft of the frame)
+  const int m = c.natural ? n : ((2 * n < N) ? 2 * n : 2 * N - 1 - 2 * n);
+  if (dense_rows) return dense_rows[(int64_t)f * N + m];
+  const int64_t t = reflect_idx((int64_t)fd.k * c.hop + m - c.ext, fd.T);
+  double s;
+  if (pcm_kind == 0) {
+    s = (double)((const int16_t*)pcm)[fd.pcm_off + t];
+    if (fd.noise_off >= 0) {
+      // sig + alp*ns, evaluated in fp64 without contraction (features.py:31)
+      const double ns = (double)noise[fd.noise_off + t];
+      s = __dadd_rn(s, __dmul_rn(fd.alpha, ns));
+    }
+  } else if (pcm_kind == 1) {
+    s = ((const double*)pcm)[fd.pcm_off + t];
+  } else {
+    // pcm_kind 2: scipy.signal.convolve(int16 s, diff kernel, 'same') -> int64, exact
+    // (computeFDLPSpectrogram.py:162-164); 'same' = full[6 : 6+T], zeros outside [0, T)
+    const int16_t* x = (const int16_t*)pcm + fd.pcm_off;
+    long long acc = 0;
+#pragma unroll
+    for (int q = 0; q < 13; ++q) {
+      const int64_t idx = t + 6 - q;
+      if (idx >= 0 && idx < fd.T) acc += (long long)kDiffTaps[q] * (long long)x[idx];
+    }
+    s = (double)acc;
+  }
+  return __dmul_rn(s, c.hamming[m]);  // frame * win (features.py:153)
+}
+
+// REAL (even N): the real sequence v of length N is packed as z[q] = v[2q] + i v[2q+1] and
+// transformed with a length-N/2 complex FFT (dft2_dct_kernel<true> unpacks); otherwise v is
+// transformed as a complex sequence of length N.  The four-step split is N1 x N2 of that length.
+template <bool REAL>
+__global__ __launch_bounds__(256) void frames_dft1_kernel(
+    DevConsts c, DftPlan d1, int N2, const void* __restrict__ pcm, int pcm_kind,
+    const int16_t* __restrict__ noise, const FrameDesc* __restrict__ frames,
+    const double* __restrict__ dense_rows, const double2* __restrict__ om1,
+    double2* __restrict__ z) {
+  extern __shared__ double2 smem[];
+  const int N1 = d1.n;
+  double2* bufA = smem;
+  double2* bufB = smem + N1 * kDftCols;
+  double2* oms = smem + 2 * N1 * kDftCols;
+  const int f = blockIdx.y;
+  const int n2_0 = blockIdx.x * kDftCols;
+  for (int q = threadIdx.x; q < N1; q += blockDim.x) oms[q] = om1[q];
+
+  FrameDesc fd;
+  if (!dense_rows) fd = frames[f];
+  // load z[N2*n1 + n2] for n1 in [0,N1), n2 in [n2_0, n2_0+kDftCols)
+  for (int e = threadIdx.x; e < N1 * kDftCols; e += blockDim.x) {
+    const int col = e % kDftCols;
+    const int n1 = e / kDftCols;
+    const int n2 = n2_0 + col;
+    double2 val = make_double2(0.0, 0.0);
+    if (n2 < N2) {
+      const int q = N2 * n1 + n2;
+      if constexpr (REAL) {
+        val.x = makhoul_sample(c, fd, 2 * q, f, pcm, pcm_kind, noise, dense_rows);
+        val.y = makhoul_sample(c, fd, 2 * q + 1, f, pcm, pcm_kind, noise, dense_rows);
+      } else {
+        val.x = makhoul_sample(c, fd, q, f, pcm, pcm_kind, noise, dense_rows);
+      }
+    }
+    bufA[n1 * kDftCols + col] = val;
+  }
+  __syncthreads();
+  double2* res = lds_dft(bufA, bufB, oms, d1, kDftCols);
+  // twiddle exp(-2 pi i n2 k1 / (N1 N2)) and store z[f][k1][n2]
+  for (int e = threadIdx.x; e < N1 * kDftCols; e += blockDim.x) {
+    const int col = e % kDftCols;
+    const int k1 = e / kDftCols;
+    const int n2 = n2_0 + col;
+    if (n2 < N2) {
+      const double2 tw = ((const double2*)c.tw1)[(int64_t)k1 * N2 + n2];
+      z[((int64_t)f * N1 + k1) * N2 + n2] = cmul(res[k1 * kDftCols + col], tw);
+    }
+  }
+}
+
+// -----------------------------------------------------------------------------------------
+// 2. row DFTs (length N2) + Makhoul post-twiddle -> DCT-II / sqrt(2N)
+//    REAL: Z = FFT_{N/2}(z) is unpacked into V = FFT_N(v) with E = (Z_k + conj Z_{M-k})/2,
+//    O = (Z_k - conj Z_{M-k})/(2i), V_k = E + w^k O, V_{k+M} = E - w^k O (w = e^{-2 pi i/N},
+//    M = N/2).  A workgroup holds rows k1 and N1-k1 (4 such pairs), so Z_{M-k} is in its LDS.
+// -----------------------------------------------------------------------------------------
+template <bool REAL>
+__global__ __launch_bounds__(256) void dft2_dct_kernel(DevConsts c, DftPlan d2, int N1,
+                                                       const double2* __restrict__ z,
+                                                       const double2* __restrict__ om2,
+                                                       double inv_scale_div, double* __restrict__ dct) {
+  extern __shared__ double2 smem[];
+  const int N2 = d2.n;
+  double2* bufA = smem;
+  double2* bufB = smem + N2 * kDftCols;
+  double2* oms = smem + 2 * N2 * kDftCols;
+  const int f = blockIdx.y;
+  const int N = c.N;
+  constexpr int kHalf = kDftCols / 2;
+  // slot -> row k1 (-1: unused).  REAL: slots r and r + 4 hold the rows of pair pp = 4 b + r,
+  // (pp, N1 - pp); a self-paired row (pp = 0 or 2 pp = N1) occupies slot r only.
+  auto slot_row = [&](int r) -> int {
+    if constexpr (REAL) {
+      const int pp = blockIdx.x * kHalf + (r % kHalf);
+      if (2 * pp > N1) return -1;
+      if (r < kHalf) return pp;
+      const int m = N1 - pp;
+      return (pp == 0 || m == pp) ? -1 : m;
+    } else {
+      const int k1 = blockIdx.x * kDftCols + r;
+      return k1 < N1 ? k1 : -1;
+    }
+  };
+  for (int q = threadIdx.x; q < N2; q += blockDim.x) oms[q] = om2[q];
+  for (int e = threadIdx.x; e < N2 * kDftCols; e += blockDim.x) {
+    const int row = e / N2;  // coalesced over n2
+    const int n2 = e % N2;
+    const int k1 = slot_row(row);
+    double2 v = make_double2(0.0, 0.0);
+    if (k1 >= 0) v = z[((int64_t)f * N1 + k1) * N2 + n2];
+    bufA[n2 * kDftCols + row] = v;
+  }
+  __syncthreads();
+  double2* res = lds_dft(bufA, bufB, oms, d2, kDftCols);
+  const double2* post = (const double2*)c.post;
+  for (int e = threadIdx.x; e < N2 * kDftCols; e += blockDim.x) {
+    const int row = e % kDftCols;
+    const int k2 = e / kDftCols;
+    const int k1 = slot_row(row);
+    if (k1 < 0) continue;
+    const int k = k1 + N1 * k2;
+    const double2 V = res[k2 * kDftCols + row];
+    if constexpr (REAL) {
+      const int M = N1 * N2;
+      // km = M - k (Z_M = Z_0) split as k1m + N1 k2m without a division
+      const int k1m = k1 == 0 ? 0 : N1 - k1;
+      const int k2m = k1 == 0 ? (k2 == 0 ? 0 : N2 - k2) : N2 - 1 - k2;
+      const int rm = k1m == k1 ? row : (row < kHalf ? row + kHalf : row - kHalf);
+      const double2 W = res[k2m * kDftCols + rm];
+      const double2 E = make_double2(0.5 * (V.x + W.x), 0.5 * (V.y - W.y));
+      const double2 O = make_double2(0.5 * (V.y + W.y), -0.5 * (V.x - W.x));
+      const double2 t = cmul(((const double2*)c.rtw)[k], O);
+      const double2 V1 = make_double2(E.x + t.x, E.y + t.y);
+      const double2 V2 = make_double2(E.x - t.x, E.y - t.y);
+      const double2 w1 = post[k], w2 = post[k + M];
+      dct[(int64_t)f * N + k] = 2.0 * (w1.x * V1.x - w1.y * V1.y) / inv_scale_div;
+      dct[(int64_t)f * N + k + M] = 2.0 * (w2.x * V2.x - w2.y * V2.y) / inv_scale_div;
+    } else if (c.natural) {
+      // complex modulation: ifft(frame)[k] = conj(DFT_k) / N (real frame), bins k < int(N/2)
+      // (computeModulationSpectrum.py:154-155); row f of N doubles holds them as double2
+      if (k < N / 2) {
+        const double inv = 1.0 / (double)N;
+        ((double2*)(dct + (int64_t)f * N))[k] = make_double2(V.x * inv, -V.y * inv);
+      }
+    } else {
+      const double2 w = post[k];
+      const double y = 2.0 * (w.x * V.x - w.y * V.y);
+      dct[(int64_t)f * N + k] = y / inv_scale_div;  // dct(.)/np.sqrt(2N)  (:178)
+    }
+  }
+}
+
+// -----------------------------------------------------------------------------------------
+// 1s/2s. The same two DCT passes specialised at compile time for the recipes' frame length
+// (N = 24000: packed length-12000 complex FFT = 100 x 120; radices 4.5.5 and 8.3.5): constant
+// butterflies (roots of unity as literals), constant Stockham strides, COLS interleaved columns
+// (rows) per workgroup, and a branch-free sample gather for frames that need no reflect padding.
+// Same arithmetic order per butterfly as the generic passes (Stockham DIT, twiddle then DFT).
+// -----------------------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ void bfly_c(double2 (&v)[R]) {
+  if constexpr (R == 2) {
+    const double2 a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = make_double2(a.x - b.x, a.y - b.y);
+  } else if constexpr (R == 4) {
+    const double2 a0 = cadd(v[0], v[2]), a1 = make_double2(v[0].x - v[2].x, v[0].y - v[2].y);
+    const double2 b0 = cadd(v[1], v[3]), b1 = make_double2(v[1].x - v[3].x, v[1].y - v[3].y);
+    const double2 b1m = make_double2(b1.y, -b1.x);  // -i b1
+    v[0] = cadd(a0, b0);
+    v[2] = make_double2(a0.x - b0.x, a0.y - b0.y);
+    v[1] = cadd(a1, b1m);
+    v[3] = make_double2(a1.x - b1m.x, a1.y - b1m.y);
+  } else if constexpr (R == 3) {
+    constexpr double c1 = -0.5, s1 = -0.86602540378443864676;  // e^{-2 pi i / 3}
+    const double2 t = cadd(v[1], v[2]);
+    const double2 d = make_double2(v[1].x - v[2].x, v[1].y - v[2].y);
+    const double2 m = make_double2(v[0].x + c1 * t.x, v[0].y + c1 * t.y);
+    const double2 u = make_double2(-s1 * d.y, s1 * d.x);  // i s1 d
+    v[0] = cadd(v[0], t);
+    v[1] = cadd(m, u);
+    v[2] = make_double2(m.x - u.x, m.y - u.y);
+  } else if constexpr (R == 5) {
+    constexpr double c1 = 0.30901699437494742410, s1 = -0.95105651629515357212;  // e^{-2 pi i / 5}
+    constexpr double c2 = -0.80901699437494742410, s2 = -0.58778525229247312917; // e^{-4 pi i / 5}
+    const double2 t1 = cadd(v[1], v[4]), d1 = make_double2(v[1].x - v[4].x, v[1].y - v[4].y);
+    const double2 t2 = cadd(v[2], v[3]), d2 = make_double2(v[2].x - v[3].x, v[2].y - v[3].y);
+    const double2 m1 = make_double2(v[0].x + c1 * t1.x + c2 * t2.x, v[0].y + c1 * t1.y + c2 * t2.y);
+    const double2 m2 = make_double2(v[0].x + c2 * t1.x + c1 * t2.x, v[0].y + c2 * t1.y + c1 * t2.y);
+    // i (s1 d1 + s2 d2) and i (s2 d1 - s1 d2)
+    const double2 u1 = make_double2(-(s1 * d1.y + s2 * d2.y), s1 * d1.x + s2 * d2.x);
+    const double2 u2 = make_double2(-(s2 * d1.y - s1 * d2.y), s2 * d1.x - s1 * d2.x);
+    v[0] = cadd(cadd(v[0], t1), t2);
+    v[1] = cadd(m1, u1);
+    v[4] = make_double2(m1.x - u1.x, m1.y - u1.y);
+    v[2] = cadd(m2, u2);
+    v[3] = make_double2(m2.x - u2.x, m2.y - u2.y);
+  }
+}
+
+// LDS slot of element (pos, col) of COLS = 8 interleaved columns.  SWZ: the column index XORed with
+// g(pos mod 8) = ((pos & 1) << 2) | ((pos & 7) >> 1), so 8 consecutive positions of one column (the
+// row pass's coalesced load order) land in 8 different 16-byte bank groups, while the 8 columns of one
+// position still fill its 128 bytes (the stage reads' lane groups pair positions p and p + 2 on
+// complementary column halves; g keeps bit 2 equal for p and p + 2, so they stay disjoint).
+template <bool SWZ>
+__device__ __forceinline__ int lslot(int pos, int col) {
+  if constexpr (SWZ) return pos * 8 + (col ^ (((pos & 1) << 2) | ((pos & 7) >> 1)));
+  else return pos * 8 + col;
+}
+
+// One Stockham stage (radix R, Ns = product of the radices before it) of COLS interleaved length-N
+// columns in LDS; om = the N roots omega_N^q.  IP (in place, in == out): every thread reads and
+// transforms all its butterflies first, then a barrier, then the writes; one buffer instead of two,
+// so twice the workgroups fit a CU's LDS (same arithmetic, bit-identical results).
+template <int N, int COLS, int NT, int Ns, int R, bool SWZ = false, bool IP = false>
+__device__ __forceinline__ void st_stage_c(const double2* __restrict__ in, double2* __restrict__ out,
+                                           const double2* __restrict__ om) {
+  static_assert(!SWZ || COLS == 8, "swizzle of 8 columns");
+  constexpr int NB = N / R, TOT = NB * COLS, ITER = (TOT + NT - 1) / NT, TW0 = N / (Ns * R);
+  const double2* src = in;
+  double2* dst = out;
+  if constexpr (IP) src = out;  // the caller passes the one buffer as out
+  auto slot = [&](int pos, int col) { return SWZ ? lslot<SWZ>(pos, col) : pos * COLS + col; };
+  double2 v[IP ? ITER : 1][R];
+#pragma unroll
+  for (int it = 0; it < ITER; ++it) {
+    const int b = (int)threadIdx.x + it * NT;
+    if (TOT % NT != 0 && b >= TOT) break;
+    const int col = b % COLS, j = b / COLS;
+    const int k = j % Ns, jq = j / Ns;
+    double2 (&w)[R] = v[IP ? it : 0];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const double2 x = src[slot(j + r * NB, col)];
+      w[r] = (r == 0 || Ns == 1) ? x : cmul(x, om[TW0 * k * r]);
+    }
+    bfly_c<R>(w);
+    if constexpr (!IP) {
+      const int idxD = jq * Ns * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) dst[slot(idxD + r * Ns, col)] = w[r];
+    }
+  }
+  if constexpr (IP) {
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int b = (int)threadIdx.x + it * NT;
+      if (TOT % NT != 0 && b >= TOT) break;
+      const int col = b % COLS, j = b / COLS;
+      const int k = j % Ns, jq = j / Ns;
+      const int idxD = jq * Ns * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) dst[slot(idxD + r * Ns, col)] = v[it][r];
+    }
+  }
+}
+
+// full length-N DFT of COLS columns, radices R0 R1 ...; returns the buffer holding the result
+// (IP: a only, b unused)
+template <int N, int COLS, int NT, bool SWZ, bool IP, int Ns, int R0, int... Rs>
+__device__ __forceinline__ double2* lds_dft_c(double2* a, double2* b, const double2* om) {
+  if constexpr (IP) {
+    st_stage_c<N, COLS, NT, Ns, R0, SWZ, true>(a, a, om);
+    __syncthreads();
+    if constexpr (sizeof...(Rs) > 0) return lds_dft_c<N, COLS, NT, SWZ, true, Ns * R0, Rs...>(a, b, om);
+    else return a;
+  } else {
+    st_stage_c<N, COLS, NT, Ns, R0, SWZ>(a, b, om);
+    __syncthreads();
+    if constexpr (sizeof...(Rs) > 0) return lds_dft_c<N, COLS, NT, SWZ, false, Ns * R0, Rs...>(b, a, om);
+    else return b;
+  }
+}
+
+#ifndef FDLP_DCT_IP
+#define FDLP_DCT_IP 1  // in-place Stockham stages in the specialised DCT kernels (0: ping-pong buffers)
+#endif
+constexpr bool kDctIP = FDLP_DCT_IP != 0;
+
+template <int N1>
+struct DctRadices1;
+template <>
+struct DctRadices1<100> {
+  template <int COLS, int NT>
+  __device__ static double2* run(double2* a, double2* b, const double2* om) {
+    return lds_dft_c<100, COLS, NT, false, kDctIP, 1, 4, 5, 5>(a, b, om);
+  }
+};
+template <int N2>
+struct DctRadices2;
+template <>
+struct DctRadices2<120> {
+  template <int COLS, int NT, bool SWZ = false>
+  __device__ static double2* run(double2* a, double2* b, const double2* om) {
+    return lds_dft_c<120, COLS, NT, SWZ, kDctIP, 1, 4, 2, 3, 5>(a, b, om);
+  }
+};
+
+template <int N1, int N2, int COLS>
+__global__ __launch_bounds__(256) void frames_dft1_c_kernel(DevConsts c, const void* __restrict__ pcm, int pcm_kind,
+                                                            const int16_t* __restrict__ noise,
+                                                            const FrameDesc* __restrict__ frames,
+                                                            const double2* __restrict__ om1,
+                                                            double2* __restrict__ z, int nframes) {
+  constexpr int NT = 256;
+  __shared__ double2 bufA[N1 * COLS], bufB[kDctIP ? 1 : N1 * COLS], oms[N1], twb[N2];
+  // 1-D grid, XCD-mapped: the column blocks of a frame run on one XCD (their z rows share L2 lines)
+  constexpr int NBX = (N2 + COLS - 1) / COLS;
+  const int it0 = xcd_item();
+  if (it0 >= nframes * NBX) return;
+  const int f = it0 / NBX;
+  const int n2_0 = (it0 - f * NBX) * COLS;
+  for (int q = threadIdx.x; q < N1; q += NT) oms[q] = om1[q];
+  // four-step twiddle W^{k1 n2} (W = e^{-2 pi i / (N1 N2)}) with k1 n2 = N2 a + b: W_{N1}^{a} W^{b}, i.e.
+  // the N1 roots (oms) times row k1 = 1 of the tw1 table (W^{b}, b < N2)
+  const double2* tw1 = (const double2*)c.tw1;
+  for (int q = threadIdx.x; q < N2; q += NT) twb[q] = tw1[N2 + q];
+  const FrameDesc fd = frames[f];
+  const int N = c.N;
+  const int64_t t0 = (int64_t)fd.k * c.hop - c.ext;
+  // no reflect padding, plain int16, no mixing: sample m of the frame is pcm[pcm_off + t0 + m]
+  const bool fast = pcm_kind == 0 && fd.noise_off < 0 && t0 >= 0 && t0 + N <= fd.T;
+  const int16_t* xs = (const int16_t*)pcm + fd.pcm_off + t0;
+  constexpr int TOT = N1 * COLS;
+#pragma unroll
+  for (int it = 0; it < (TOT + NT - 1) / NT; ++it) {
+    const int e = (int)threadIdx.x + it * NT;
+    if (TOT % NT != 0 && e >= TOT) break;
+    const int col = e % COLS, n1 = e / COLS;
+    const int q = N2 * n1 + n2_0 + col;  // packed z[q] = v[2q] + i v[2q+1] (Makhoul order v)
+    const int m0 = 4 * q < N ? 4 * q : 2 * N - 1 - 4 * q;
+    const int m1 = 4 * q + 2 < N ? 4 * q + 2 : 2 * N - 3 - 4 * q;
+    double2 val;
+    if (fast) {
+      val.x = __dmul_rn((double)xs[m0], c.hamming[m0]);
+      val.y = __dmul_rn((double)xs[m1], c.hamming[m1]);
+    } else {
+      val.x = makhoul_sample(c, fd, 2 * q, f, pcm, pcm_kind, noise, nullptr);
+      val.y = makhoul_sample(c, fd, 2 * q + 1, f, pcm, pcm_kind, noise, nullptr);
+    }
+    bufA[n1 * COLS + col] = val;
+  }
+  __syncthreads();
+  const double2* res = DctRadices1<N1>::template run<COLS, NT>(bufA, bufB, oms);
+#pragma unroll
+  for (int it = 0; it < (TOT + NT - 1) / NT; ++it) {
+    const int e = (int)threadIdx.x + it * NT;
+    if (TOT % NT != 0 && e >= TOT) break;
+    const int col = e % COLS, k1 = e / COLS;
+    const int n2 = n2_0 + col;
+    const int q = k1 * n2;  // < N1 N2
+    const double2 tw = cmul(oms[q / N2], twb[q % N2]);
+    z[((int64_t)f * N1 + k1) * N2 + n2] = cmul(res[k1 * COLS + col], tw);
+  }
+}
+
+// rows k1 of pair pp (pp, N1 - pp): slots r (< COLS/2) and r + COLS/2
+template <int N1, int N2, int COLS, bool TWF = true, bool SWZ = true>
+__global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const double2* __restrict__ z,
+                                                         const double2* __restrict__ om2, double scale2,
+                                                         double* __restrict__ dct, int nframes) {
+  // scale2 = 2 / sqrt(2N): dct(.) / np.sqrt(2N) (:178) as one multiplication (within an ulp of the
+  // reference's division; no fp64 division per coefficient)
+  constexpr int NT = 256, HALF = COLS / 2;
+  __shared__ double2 bufA[N2 * COLS], bufB[kDctIP ? 1 : N2 * COLS], oms[N2];
+  __shared__ double2 pw1[N1], pw2[N2], rw1[N1], rw2[N2];  // factored twiddles (TWF)
+  // 1-D grid, XCD-mapped: the row-pair blocks of a frame run on one XCD, so the 32-B runs they store
+  // into each D line (k = k1 + N1 k2: 4 consecutive k1 per block) merge in that XCD's L2
+  constexpr int NBX = (N1 / 2 + 1 + HALF - 1) / HALF;
+  const int it0 = xcd_item();
+  if (it0 >= nframes * NBX) return;
+  const int f = it0 / NBX;
+  const int bx = it0 - f * NBX;
+  const int N = c.N;
+  auto slot_row = [&](int r) -> int {
+    const int pp = bx * HALF + (r % HALF);
+    if (2 * pp > N1) return -1;
+    if (r < HALF) return pp;
+    const int m = N1 - pp;
+    return (pp == 0 || m == pp) ? -1 : m;
+  };
+  for (int q = threadIdx.x; q < N2; q += NT) oms[q] = om2[q];
+  if (TWF) {  // post[k] = post[k1] post[N1 k2], rtw[k] = rtw[k1] rtw[N1 k2]  (k = k1 + N1 k2)
+    const double2* post = (const double2*)c.post;
+    const double2* rtw = (const double2*)c.rtw;
+    for (int q = threadIdx.x; q < N1; q += NT) { pw1[q] = post[q]; rw1[q] = rtw[q]; }
+    for (int q = threadIdx.x; q < N2; q += NT) { pw2[q] = post[N1 * q]; rw2[q] = rtw[N1 * q]; }
+  }
+  constexpr int TOT = N2 * COLS;
+#pragma unroll
+  for (int it = 0; it < (TOT + NT - 1) / NT; ++it) {
+    const int e = (int)threadIdx.x + it * NT;
+    if (TOT % NT != 0 && e >= TOT) break;
+    const int row = e / N2, n2 = e % N2;  // coalesced over n2 (the row-fastest order measured slower)
+    const int k1 = slot_row(row);
+    double2 v = make_double2(0.0, 0.0);
+    if (k1 >= 0) v = z[((int64_t)f * N1 + k1) * N2 + n2];
+    bufA[lslot<SWZ>(n2, row)] = v;
+  }
+  __syncthreads();
+  const double2* res = DctRadices2<N2>::template run<COLS, NT, SWZ>(bufA, bufB, oms);
+  const double2* post = (const double2*)c.post;
+  const double2* rtw = (const double2*)c.rtw;
+  constexpr int M = N1 * N2;
+#pragma unroll
+  for (int it = 0; it < (TOT + NT - 1) / NT; ++it) {
+    const int e = (int)threadIdx.x + it * NT;
+    if (TOT % NT != 0 && e >= TOT) break;
+    const int row = e % COLS, k2 = e / COLS;
+    const int k1 = slot_row(row);
+    if (k1 < 0) continue;
+    const int k = k1 + N1 * k2;
+    const double2 V = res[lslot<SWZ>(k2, row)];
+    const int k1m = k1 == 0 ? 0 : N1 - k1;
+    const int k2m = k1 == 0 ? (k2 == 0 ? 0 : N2 - k2) : N2 - 1 - k2;
+    const int rm = k1m == k1 ? row : (row < HALF ? row + HALF : row - HALF);
+    const double2 W = res[lslot<SWZ>(k2m, rm)];
+    const double2 E = make_double2(0.5 * (V.x + W.x), 0.5 * (V.y - W.y));
+    const double2 O = make_double2(0.5 * (V.y + W.y), -0.5 * (V.x - W.x));
+    double2 rt, w1, w2;
+    if (TWF) {
+      rt = cmul(rw1[k1], rw2[k2]);
+      w1 = cmul(pw1[k1], pw2[k2]);
+      // post[k + M] = post[k] e^{-i pi M / (2N)} = post[k] e^{-i pi / 4}  (M = N / 2)
+      constexpr double h = 0.70710678118654752440;
+      w2 = make_double2(h * (w1.x + w1.y), h * (w1.y - w1.x));
+    } else {
+      rt = rtw[k];
+      w1 = post[k];
+      w2 = post[k + M];
+    }
+    const double2 t = cmul(rt, O);
+    const double2 V1 = make_double2(E.x + t.x, E.y + t.y);
+    const double2 V2 = make_double2(E.x - t.x, E.y - t.y);
+    dct[(int64_t)f * N + k] = (w1.x * V1.x - w1.y * V1.y) * scale2;
+    dct[(int64_t)f * N + k + M] = (w2.x * V2.x - w2.y * V2.y) * scale2;
+  }
+}
+
+// -----------------------------------------------------------------------------------------
+// launch wrappers
+// -----------------------------------------------------------------------------------------
+hipError_t launch_frames_dft1(const DevConsts& c, const DftPlan& d1, int N2, const void* pcm,
+                              int pcm_kind, const int16_t* noise, const FrameDesc* frames,
+                              const double* dense_rows, int nframes, double2* z, const double2* om1,
+                              hipStream_t s) {
+  if (nframes <= 0) return hipSuccess;
+  dim3 grid((N2 + kDftCols - 1) / kDftCols, nframes);
+  size_t lds = sizeof(double2) * (2 * d1.n * kDftCols + d1.n);
+  if (c.real_fft && d1.n == 100 && N2 == 120 && !dense_rows) {  // recipes: N = 24000
+    hipLaunchKernelGGL((frames_dft1_c_kernel<100, 120, kDftCols>), dim3(xcd_grid(grid.x * nframes)), dim3(256), 0, s, c,
+                       pcm, pcm_kind, noise, frames, om1, z, nframes);
+    return hipGetLastError();
+  }
+  if (c.real_fft) {
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)frames_dft1_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(frames_dft1_kernel<true>, grid, dim3(256), lds, s, c, d1, N2, pcm, pcm_kind, noise,
+                       frames, dense_rows, om1, z);
+  } else {
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)frames_dft1_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(frames_dft1_kernel<false>, grid, dim3(256), lds, s, c, d1, N2, pcm, pcm_kind, noise,
+                       frames, dense_rows, om1, z);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const double2* z,
+                           int nframes, double* dct, const double2* om2, hipStream_t s) {
+  if (nframes <= 0) return hipSuccess;
+  size_t lds = sizeof(double2) * (2 * d2.n * kDftCols + d2.n);
+  const double div = sqrt((double)(2 * c.N));
+  if (c.real_fft && N1 == 100 && d2.n == 120) {  // recipes: N = 24000
+    dim3 grid((N1 / 2 + 1 + kDftCols / 2 - 1) / (kDftCols / 2), nframes);
+    const dim3 g1(xcd_grid(grid.x * nframes));
+    const double sc2 = 2.0 / div;
+    hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, true>), g1, dim3(256), 0, s, c, z, om2, sc2, dct, nframes);
+    return hipGetLastError();
+  }
+  if (c.real_fft) {
+    dim3 grid((N1 / 2 + 1 + kDftCols / 2 - 1) / (kDftCols / 2), nframes);  // row pairs (k1, N1-k1)
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)dft2_dct_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(dft2_dct_kernel<true>, grid, dim3(256), lds, s, c, d2, N1, z, om2, div, dct);
+  } else {
+    dim3 grid((N1 + kDftCols - 1) / kDftCols, nframes);
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)dft2_dct_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(dft2_dct_kernel<false>, grid, dim3(256), lds, s, c, d2, N1, z, om2, div, dct);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace fdlp

@@ -1,0 +1,217 @@
+// fdlp_device.h -- device-side helpers shared by the gfx950 kernel translation units
+// (fdlp_dct.hip, fdlp_autocorr.hip, fdlp_lpc.hip, fdlp_misc.hip): complex arithmetic and the LDS
+// Stockham DFT, the XCD-aware grid mapping, wave / DPP-row reductions, DPP-broadcast FMAs and the
+// counted LDS loads.  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "fdlp_internal.h"
+
+namespace fdlp {
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// -----------------------------------------------------------------------------------------
+// complex helpers
+// -----------------------------------------------------------------------------------------
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+
+// R-point forward DFT in registers; roots from the length-n table (omega_n^q), stride n/R.
+template <int R>
+__device__ __forceinline__ void small_dft(double2* v, const double2* __restrict__ om, int n) {
+  if constexpr (R == 2) {
+    double2 a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = make_double2(a.x - b.x, a.y - b.y);
+  } else if constexpr (R == 4) {
+    double2 a0 = cadd(v[0], v[2]), a1 = make_double2(v[0].x - v[2].x, v[0].y - v[2].y);
+    double2 b0 = cadd(v[1], v[3]), b1 = make_double2(v[1].x - v[3].x, v[1].y - v[3].y);
+    // forward: multiply b1 by -i
+    double2 b1m = make_double2(b1.y, -b1.x);
+    v[0] = cadd(a0, b0);
+    v[2] = make_double2(a0.x - b0.x, a0.y - b0.y);
+    v[1] = cadd(a1, b1m);
+    v[3] = make_double2(a1.x - b1m.x, a1.y - b1m.y);
+  } else {
+    double2 out[R];
+    const int st = n / R;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      double2 acc = v[0];
+#pragma unroll
+      for (int p = 1; p < R; ++p) acc = cadd(acc, cmul(v[p], om[((p * q) % R) * st]));
+      out[q] = acc;
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) v[q] = out[q];
+  }
+}
+
+// One Stockham autosort stage of radix R over `ncols` interleaved columns of length n.
+// in/out index = pos * ncols + col.  Ns = product of the radices already applied.
+template <int R>
+__device__ inline void stockham_stage(const double2* __restrict__ in, double2* __restrict__ out,
+                               const double2* __restrict__ om, int n, int ncols, int Ns) {
+  const int nb = n / R;
+  const int total = nb * ncols;
+  const int tw0 = n / (Ns * R);
+  const float inv_ns = 1.0f / (float)Ns;
+  for (int b = threadIdx.x; b < total; b += blockDim.x) {
+    const int col = b % ncols;
+    const int j = b / ncols;
+    // j / Ns without an integer division (j < 512: the float quotient is off by at most one)
+    int jq = (int)((float)j * inv_ns);
+    jq += (jq + 1) * Ns <= j;
+    jq -= jq * Ns > j;
+    const int k = j - jq * Ns;
+    double2 v[R];
+    const int twstep = tw0 * k;  // omega_{Ns*R}^{k*r} = omega_n^{k*r*n/(Ns*R)}; twstep * r < n
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      double2 x = in[(j + r * nb) * ncols + col];
+      v[r] = (r == 0) ? x : cmul(x, om[twstep * r]);
+    }
+    small_dft<R>(v, om, n);
+    const int idxD = jq * Ns * R + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) out[(idxD + r * Ns) * ncols + col] = v[r];
+  }
+}
+
+// Full length-n DFT of ncols columns resident in LDS (ping-pong a <-> b).  Returns the buffer
+// holding the result.
+__device__ inline double2* lds_dft(double2* a, double2* b, const double2* om, const DftPlan& d, int ncols) {
+  int Ns = 1;
+  for (int s = 0; s < d.nrad; ++s) {
+    const int R = d.rad[s];
+    switch (R) {
+      case 2: stockham_stage<2>(a, b, om, d.n, ncols, Ns); break;
+      case 3: stockham_stage<3>(a, b, om, d.n, ncols, Ns); break;
+      case 4: stockham_stage<4>(a, b, om, d.n, ncols, Ns); break;
+      case 5: stockham_stage<5>(a, b, om, d.n, ncols, Ns); break;
+      case 7: stockham_stage<7>(a, b, om, d.n, ncols, Ns); break;
+      default: break;  // rejected at plan creation
+    }
+    __syncthreads();
+    Ns *= R;
+    double2* t = a; a = b; b = t;
+  }
+  return a;
+}
+
+constexpr int kDftCols = 8;     // columns (rows) per workgroup in the two DFT passes
+
+// Workgroup b is dispatched to XCD b % 8.  Giving every XCD a contiguous run of work items keeps
+// the items that read the same frame (its D row) on one L2 instead of pulling the row into all
+// eight.  Grid = 8 * ceil(total / 8); the padding workgroups get an index >= total.
+constexpr int kXcds = 8;
+__device__ __forceinline__ int xcd_item() {
+  const int per = gridDim.x / kXcds;
+  return (int)(blockIdx.x % kXcds) * per + (int)(blockIdx.x / kXcds);
+}
+static inline int xcd_grid(int total) { return (total + kXcds - 1) / kXcds * kXcds; }
+
+// -----------------------------------------------------------------------------------------
+// wave-level helpers
+// -----------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// -----------------------------------------------------------------------------------------
+// 16-lane (one DPP row) helpers: an item is owned by a row of 16 lanes, 4 items per wave.
+// -----------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  // every control used here has an in-row source for every lane, so no 'old' value is needed
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// sum over the 16 lanes of a DPP row; every lane gets the same (bitwise) value
+__device__ __forceinline__ double row_sum16(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x140>(v);  // row_mirror
+  return v;
+}
+__device__ __forceinline__ void wave_lds_sync() {
+  // LDS ops of one wave complete in order; this only stops the compiler from reordering
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 8-lane (half DPP row) sum; every lane of the half gets the same (bitwise) value
+__device__ __forceinline__ double sum8(double v) {  // over the 8 lanes of a half DPP row
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror: lane i <-> 7-i inside each 8-lane half
+  return v;
+}
+
+template <int K>
+__device__ __forceinline__ double row_bcast(double v) {
+  // row_newbcast:K; every lane has a source, and bound_ctrl spares the 'old' operand (no init, no nops)
+  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + K, 0xF, 0xF, true);
+}
+
+// acc += s[n0+V] * w with s[n0+V] read from lane V of the row by the FMA itself (DP ALU DPP:
+// v_fmac_f64 takes row_newbcast on its first source), so a block costs A^2 FMAs and no moves
+template <int V>
+__device__ __forceinline__ void fmac_bcast(double& acc, double cur, double w) {
+  asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(cur), "v"(w), "n"(V));
+}
+
+// LDS read of one double at a compile-time byte offset from a per-lane byte address.  Plain
+// ds_read_b64 (2 LDS cycles per wave when conflict-free); the compiler would otherwise merge the
+// window into ds_read2_b64 / ds_read_b128, which run at half rate or 2-way conflicted here.
+// The caller waits with lds_wait() before using the values.
+template <int OFF>
+__device__ __forceinline__ double lds_ld(uint32_t addr) {
+  double v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// 16 alpha values alpha[OFF - j] (j < 16, byte offsets from the lane's LDS address `addr`) as single
+// ds_read_b64: 2 LDS cycles per wave-instruction, where the compiler's merged ds_read2_b64 takes 8 for
+// two (MI355X_MICROARCH.md LDS table).  The asm results look ready to the compiler, so the caller
+// waits (lgkm_wait) before the FMAs that read them.
+template <int OFF, int J = 0>
+__device__ __forceinline__ void lds_load16(double (&v)[16], uint32_t addr) {
+  if constexpr (J < 16) {
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v[J]) : "v"(addr), "i"(8 * (OFF - J)) : "memory");
+    lds_load16<OFF, J + 1>(v, addr);
+  }
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory"); }
+
+// numpy 'reflect' padding index (getFrames, features.py:146)
+__device__ __forceinline__ int64_t reflect_idx(int64_t q, int64_t T) {
+  // numpy 'reflect' pad == periodic reflection with period 2(T-1) (features.py:146); the 64-bit
+  // modulo is only needed when the pad exceeds one period (utterances shorter than the padding)
+  if (q >= 0 && q < T) return q;
+  if (T == 1) return 0;
+  const int64_t P = 2 * (T - 1);
+  if (q < 0 && q > -T) return -q;
+  if (q >= T && q < P) return P - q;
+  q %= P;
+  if (q < 0) q += P;
+  return q < T ? q : P - q;
+}
+
+// the --add_noise diff filter (static: one copy per translation unit)
+static __constant__ int kDiffTaps[13] = {1, 2, 3, 2, 0, -2, -5, -2, 0, 2, 3, 2, 1};  // :163
+
+}  // namespace fdlp

@@ -1,5 +1,5 @@
 // fdlp_internal.h -- structures shared by the host runtime (fdlp_plan.cpp) and the gfx950
-// kernels (fdlp_kernels.hip).  Not part of the public ABI.
+// kernels (fdlp_*.hip).  Not part of the public ABI.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -36,7 +36,7 @@ struct UttDesc {
 };
 
 // One snapshot of a skirt sweep: after the positions >= S are consumed, band `band` receives
-// K times the truncated autocorrelation (structured autocorrelation, fdlp_kernels.hip 3s).
+// K times the truncated autocorrelation (structured autocorrelation, fdlp_autocorr.hip 3s).
 struct SkSnap {
   int32_t S;
   int32_t band;
@@ -84,21 +84,18 @@ struct DevConsts {
   const int2* fl_band = nullptr;  // [B] (chain, bitmask of the parts h < fl_H - 1 it needs a partial from)
   // persistent LPC kernel: resident blocks on the plan's device (prepare_lpc_env, at plan creation)
   int lpc_blocks = 0;
-  int lpc_lds_durbin = 0;  // FDLP_LPC_LDS at plan creation: the LDS Durbin instead of the lattice
-  int lpc_cep_lds = 0;     // FDLP_CEP_LDS at plan creation: the LDS cepstrum form for every M
-  int lpc_slotmajor = 0;   // FDLP_LPC_SLOTMAJOR at plan creation: the slot-major lattice Durbin
+  int lpc_mode = 0;        // fdlp_set_lpc_path: 0 lattice kernels (default), 1 the LDS Durbin (cross-check)
   int lpc_split = 0;       // the Durbin as durbin8_kernel (8 lanes per item), then the cepstrum/envelope
-                           // kernel; off with FDLP_LPC_FUSED=1 (set by prepare_lpc_env)
+                           // kernel (set by prepare_lpc_env when p fits durbin8_kernel)
   int natural = 0;         // complex modulation: frames in sample order, dft2 writes X = conj(DFT_N)/N
                            // (scipy.fftpack.ifft of the real frame), bins [0, N/2), as double2 rows of N doubles
   int lpc_astride = 0;     // split Durbin: row stride of a_pad (the cepstrum kernel's a-area length,
                            // zero past p), so a row is one contiguous LDS-DMA copy
-  int dct_generic = 0;     // FDLP_DCT_GENERIC at plan creation: runtime-radix DCT passes for every N
 };
 
 }  // namespace fdlp
 
-// Launch wrappers implemented in fdlp_kernels.hip (host-callable).
+// Launch wrappers implemented in fdlp_{dct,autocorr,lpc,misc}.hip (host-callable).
 namespace fdlp {
 struct Workspace {
   double2* z;      // [F, N1, N2] complex (four-step intermediate)
@@ -137,9 +134,6 @@ int lpc_env_region(int p, int M);
 // attribute and stores the resident block count in c.lpc_blocks.
 hipError_t prepare_lpc_env(DevConsts& c);
 int autocorr_tiles(int nlags);
-int band_fused_fits(int nlags, int p, int M, int kk);
-hipError_t launch_band_fused(const DevConsts& c, int odd_zero, const double* dct, int items, double* r_dbg,
-                             double* env, hipStream_t s);
 constexpr int kDftMaxSub = 512;  // longest LDS-resident sub-DFT of the four-step DCT
 // Complex modulation spectrum (computeModulationSpectrum.py --complex_modulation): per (frame, band) the
 // complex circular autocorrelation of W_j X (lags 0..p+1), then Hermitian Levinson, complex gain and

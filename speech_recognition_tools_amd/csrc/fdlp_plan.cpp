@@ -218,7 +218,7 @@ void flat_events(SkirtTables* T, int B) {
     if (ok) {
       T->fl = ev;
       T->fl_C = C;
-      flat_parts(T, B, getenv("FDLP_FLAT_PARTS") ? std::max(1, std::min(fdlp::kMaxFlatParts, atoi(getenv("FDLP_FLAT_PARTS")))) : 2);
+      flat_parts(T, B, 2);  // two position parts (3 and 4 measured slower)
       return;
     }
   }
@@ -359,8 +359,7 @@ struct fdlp_plan {
   // optional per-stage HIP-event timing (fdlp_set_profiling / fdlp_stage_times)
   bool profiling = false;
   bool debug_intermediates = false;  // keep a/gg/cep of the fused LPC kernel for fdlp_debug_fetch
-  bool fused = false;                // autocorrelation + LPC tail in one kernel (FDLP_FUSE_TAIL=1)
-  int pipeline = 1;                  // sub-batches alternated over two streams (FDLP_PIPELINE)
+  int pipeline = 1;                  // sub-batches alternated over two streams (fdlp_set_pipeline)
   hipStream_t aux_stream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool sk_avail = false;             // structured autocorrelation possible for this filterbank
@@ -635,10 +634,8 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   p->sk_avail = sk_ok;
   p->vs_avail = p->sk_avail && p->sk.fl_C > 0 && fdlp::vsweep_chains(p->sk.fl_C) > 0 &&
                 fdlp::vsweep_lanes_lags(p->nlags) > 0;
-  p->ac_path = !p->sk_avail || getenv("FDLP_AUTOCORR_DIRECT") ? FDLP_AC_DIRECT
-               : (p->vs_avail && !getenv("FDLP_SWEEP_MFMA")) ? FDLP_AC_STRUCTURED
-                                                              : FDLP_AC_STRUCTURED_MFMA;
-  if (const char* e = getenv("FDLP_PIPELINE")) p->pipeline = std::max(1, atoi(e));
+  // the other paths are selected explicitly (fdlp_set_autocorr_path), never from the environment
+  p->ac_path = !p->sk_avail ? FDLP_AC_DIRECT : p->vs_avail ? FDLP_AC_STRUCTURED : FDLP_AC_STRUCTURED_MFMA;
 
   // modulation weights (:94-118)
   const int M = p->M;
@@ -677,8 +674,6 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   const int N = p->N;
 
   p->max_frames = c.max_frames;
-  // the fused autocorr+LPC-tail kernel measured slower (35.7 vs 25.5+3.9 ms, r01); opt-in only
-  p->fused = fdlp::band_fused_fits(p->nlags, p->p, p->M, p->kk) != 0 && getenv("FDLP_FUSE_TAIL") != nullptr;
   if (device < 0) {  // host-only plan: geometry, filterbank, weights and OLA tables, no compute
     *out = p;
     return FDLP_OK;
@@ -730,7 +725,6 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
     }
   }
 
-  d.dct_generic = getenv("FDLP_DCT_GENERIC") != nullptr;
   // launch geometry of the persistent LPC kernel for this device (occupancy, large-LDS attribute)
   if (fdlp::prepare_lpc_env(d) != hipSuccess) PLAN_FAIL(FDLP_E_HIP, "LPC kernel launch setup failed");
 
@@ -942,12 +936,6 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
                           ? p->r_flat_part + (size_t)f0 * (p->sk.fl_H - 1) * fdlp::kMaxChains * nl
                           : nullptr;
       HIP_TRY(fdlp::launch_autocorr_structured(p->dc, p->ws.dct + f0 * N, n, r, p->r_up + it0 * nl, rflat, rpart, st));
-    } else if (p->fused && !p->debug_intermediates && !p->modspec) {
-      // autocorrelation + LPC tail in one launch (stage 3 is then empty)
-      HIP_TRY(fdlp::launch_band_fused(p->dc, p->cfg.odd_mod_zero, p->ws.dct + f0 * N, its, r, env, st));
-      HIP_TRY(mark(3));
-      HIP_TRY(mark(4));
-      return FDLP_OK;
     } else {
       HIP_TRY(fdlp::launch_autocorr(p->dc, p->ws.dct + f0 * N, nullptr, its, r, st));
     }
@@ -1029,6 +1017,20 @@ int fdlp_plan_regions(const fdlp_plan* p, int32_t* m1, int32_t* m2) {
     if (m1) m1[j] = p->sk.reg[j].x;
     if (m2) m2[j] = p->sk.reg[j].y;
   }
+  return FDLP_OK;
+}
+
+int fdlp_set_lpc_path(fdlp_plan* p, int32_t path) {
+  if (!p || (path != FDLP_LPC_AUTO && path != FDLP_LPC_LDS))
+    return fail(FDLP_E_INVALID, "fdlp_set_lpc_path: need a plan and FDLP_LPC_AUTO or FDLP_LPC_LDS");
+  if (p->device < 0) return fail(FDLP_E_INVALID, "fdlp_set_lpc_path: host-only plan");
+  DeviceGuard dg(p->device);
+  if (dg.status() != hipSuccess) return fail(FDLP_E_HIP, "hipSetDevice failed");
+  p->dc.lpc_mode = path == FDLP_LPC_LDS ? 1 : 0;
+  if (fdlp::prepare_lpc_env(p->dc) != hipSuccess) return fail(FDLP_E_HIP, "LPC kernel launch setup failed");
+  if (p->dc.lpc_split && !p->ws.a_pad &&
+      hipMalloc((void**)&p->ws.a_pad, sizeof(double) * (size_t)p->max_frames * p->B * p->dc.lpc_astride) != hipSuccess)
+    return fail(FDLP_E_NOMEM, "device workspace allocation failed");
   return FDLP_OK;
 }
 

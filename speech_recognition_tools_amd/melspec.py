@@ -4,7 +4,7 @@ run_melspec baseline the FDLP features are compared with.
 
 Per frame (getFrames, features.py:118-154, np.hamming window): log10(|fft(frame, nfft)[:nfft/2+1]| @ fbank.T)
 ('log') or its square ('power').  One plan per configuration (filterbank, window, FFT tables resident in
-HBM); mel_kernel (fdlp_kernels.hip 10) does frame gather, real FFT in LDS, magnitude, projection and log.
+HBM); mel_kernel (fdlp_misc.hip) does frame gather, real FFT in LDS, magnitude, projection and log.
 """
 import ctypes
 from dataclasses import dataclass

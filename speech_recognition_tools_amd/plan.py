@@ -260,6 +260,13 @@ class FdlpPlan:
     def set_autocorr_path(self, path: str = "auto"):
         check(lib.fdlp_set_autocorr_path(self._h, self.AUTOCORR_PATHS[path]))
 
+    LPC_PATHS = {"auto": 0, "lds": 1}
+
+    def set_lpc_path(self, path: str = "auto"):
+        """'auto': the lattice kernels (durbin8_kernel + register cepstrum / envelope); 'lds': the LDS
+        Durbin kernel (the large-p fallback, an independent cross-check)."""
+        check(lib.fdlp_set_lpc_path(self._h, self.LPC_PATHS[path]))
+
     def regions(self):
         """(m1, m2) int32 arrays: band j's lower skirt [0,m1), flat top [m1,m2), upper skirt [m2,N)."""
         m1 = np.empty(self.B, dtype=np.int32)

@@ -43,11 +43,12 @@ def _batch_inputs(meta, sig, z):
     return pcm, kw
 
 
-def run_gpu(meta, sig, z, support_eps=None, max_frames=256, debug=False, path="auto"):
+def run_gpu(meta, sig, z, support_eps=None, max_frames=256, debug=False, path="auto", lpc="auto"):
     from speech_recognition_tools_amd import FdlpPlan, PyRandom
     cfg = feature_cfg(meta, support_eps)
     plan = FdlpPlan(cfg, device=0, max_frames=max_frames)
     plan.set_autocorr_path(path)
+    plan.set_lpc_path(lpc)
     if debug:
         plan.set_debug(True)
     utts = meta["utts"]
@@ -232,11 +233,10 @@ def test_dct_rows_even_and_odd_lengths(fduration):
 @pytest.mark.parametrize("name", ["wsj", "reverb", "cli_default_mel"])
 def test_lattice_durbin_matches_lds_durbin(name, monkeypatch):
     """The register-resident lattice Durbin (default for order <= 255) and the LDS Durbin
-    (fallback for larger orders, forced here by FDLP_LPC_LDS) give the same features and a."""
+    (fallback for larger orders, selected here by fdlp_set_lpc_path) give the same features and a."""
     meta, sig, ref, z = load_golden(name)
     plan, res_lat = run_gpu(meta, sig, z)
-    monkeypatch.setenv("FDLP_LPC_LDS", "1")
-    _, res_lds = run_gpu(meta, sig, z)
+    _, res_lds = run_gpu(meta, sig, z, lpc="lds")
     for u in meta["utts"]:
         a, b = res_lat[u][0], res_lds[u][0]
         fin = np.isfinite(b)
