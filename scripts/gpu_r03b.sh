@@ -15,7 +15,7 @@ for c in ${BENCH_CONFIGS:-wsj reverb}; do
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], round(d['value'],1), 'one', round(d['one_batch_in_flight']['value'],1), r['stage'], round(r['frac'],3), {k: round(v,3) for k,v in d['stage_ms_per_step'].items()})" $O/bench_$c.json $c
 done
 [ -n "${NO_PMC:-}" ] && exit 0
-export SKIP_BENCH=1 EXTRA_PMC="SQ_WAIT_INST_LDS+SQ_INSTS_SALU+SQ_WAIT_ANY+SQ_BUSY_CYCLES+SQ_WAVE_CYCLES+SQ_WAVES"
+export SKIP_BENCH=1 EXTRA_PMC="SQ_WAIT_INST_LDS+SQ_INSTS_SALU+SQ_WAIT_ANY+SQ_BUSY_CYCLES+SQ_WAVE_CYCLES+SQ_LDS_IDX_ACTIVE"
 TAG=${TAG_PREFIX:-r03b}_reverb BENCH_ARGS="--config reverb --steps 5 --warmup 1 --no-cpu-baseline --inflight 1 --no-transfers" bash scripts/round_evidence.sh || exit 5
 TAG=${TAG_PREFIX:-r03b} BENCH_ARGS="--steps 5 --warmup 1 --no-cpu-baseline --inflight 1 --no-transfers" bash scripts/round_evidence.sh || exit 6
 for t in ${TAG_PREFIX:-r03b}_reverb ${TAG_PREFIX:-r03b}; do
