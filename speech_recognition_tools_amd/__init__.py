@@ -1,12 +1,27 @@
 """MI355X-native FDLP-spectrogram extractor (drop-in for the FDLP path of
 sadhusamik/speech_recognition_tools: src/featgen/computeFDLPSpectrogram.py + features.py).
 
-The compute path is libfdlp_hip.so (hand-written gfx950 HIP kernels behind include/fdlp.h);
-importing this package fails loudly when that library is missing.
+The compute path is libfdlp_hip.so (hand-written gfx950 HIP kernels behind include/fdlp.h); loading it
+fails loudly when the library is missing (there is no fallback).  The names below load lazily, so the
+native JOB runner of compute-fdlp-feats can choose the HIP runtime before the library is loaded
+(speech_recognition_tools_amd._hip_runtime); a process that has imported torch gets
+torch.ops.fdlp.spectrogram registered on import.
 """
-from ._lib import FdlpError, lib  # noqa: F401
-from .plan import DEFAULT_SUPPORT_EPS, FdlpPlan, FeatureConfig  # noqa: F401
-from .rng import NpRandom, PyRandom  # noqa: F401
-from . import ops  # noqa: F401,E402  (registers torch.ops.fdlp.spectrogram)
+import importlib
+import sys
+
+_LAZY = {"FdlpPlan": ".plan", "FeatureConfig": ".config", "DEFAULT_SUPPORT_EPS": ".config",
+         "PyRandom": ".rng", "NpRandom": ".rng", "FdlpError": "._lib", "lib": "._lib"}
 
 __all__ = ["FdlpPlan", "FeatureConfig", "PyRandom", "NpRandom", "FdlpError", "DEFAULT_SUPPORT_EPS"]
+
+
+def __getattr__(name):
+    mod = _LAZY.get(name)
+    if mod is None:
+        raise AttributeError("module %r has no attribute %r" % (__name__, name))
+    return getattr(importlib.import_module(mod, __name__), name)
+
+
+if "torch" in sys.modules:  # torch users: the library on torch's runtime, the custom op registered
+    from . import ops  # noqa: F401,E402

@@ -8,8 +8,13 @@ There is no fallback: if the library is missing the import raises.
 """
 import ctypes
 import os
+import sys
 
-import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+from . import _hip_runtime
+
+if _hip_runtime.TORCH or "torch" in sys.modules:
+    import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+TORCH_RUNTIME = "torch" in sys.modules  # the library shares torch's HIP runtime
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FDLP_LIB", os.path.join(_PKG, "lib", "libfdlp_hip.so"))

@@ -23,8 +23,6 @@ import numpy as np
 if __package__ in (None, ""):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
-from speech_recognition_tools_amd.featgen import features  # noqa: E402
-from speech_recognition_tools_amd.featgen.features import add_noise_to_wav_params, load_noise  # noqa: E402
 
 
 def build_parser():
@@ -100,8 +98,8 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
     the ark) unless return_feats is False (the CLI: features are streamed to the ark only)."""
     if window is not np.hamming:
         raise ValueError("only the reference's np.hamming analysis window is supported")
-    import torch
-    from speech_recognition_tools_amd import FdlpPlan, FeatureConfig, NpRandom, PyRandom
+    from speech_recognition_tools_amd.config import FeatureConfig
+    from speech_recognition_tools_amd.featgen.features import add_noise_to_wav_params, load_noise
 
     wavs, scp_type, outfile = args.scp, args.scp_type, args.outfile
     add_noise, add_reverb = args.add_noise, args.add_reverb
@@ -136,6 +134,8 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
     device = resolve_device(args)
     if getattr(args, 'host_runner', 'python') == 'native' and rir is None and not return_feats:
         return _run_native(args, cfg, device, noise, snr if noise is not None else 0.0, diff)
+    import torch
+    from speech_recognition_tools_amd import FdlpPlan, NpRandom, PyRandom
     torch.cuda.set_device(device)
     plan = FdlpPlan(cfg, device=device, max_frames=max(int(args.batch_frames), 1))
     jit_rng = PyRandom(args.seed)
@@ -330,8 +330,17 @@ def _run_native(args, cfg, device, noise, snr, diff):
 LAST_JOB_STATS = None  # fdlp_job_stats of the last native run (benchmarks/cli_throughput.py reports it)
 
 
+def native_eligible(args, return_feats=False):
+    """getFeats runs the native JOB runner (no torch object anywhere): the default host runner, no
+    --add_reverb (its device convolution goes through torch tensors), features streamed to the ark."""
+    return args.host_runner == 'native' and args.add_reverb in (None, '', 'clean') and not return_feats
+
+
 def main(argv=None):
     args = build_parser().parse_args(argv)
+    if native_eligible(args) and "torch" not in sys.modules:
+        from speech_recognition_tools_amd import _hip_runtime
+        _hip_runtime.TORCH = False  # before anything loads libfdlp_hip.so: a cold JOB skips importing torch
     start_time = time.time()
     print('%s: Extracting features....' % sys.argv[0])
     sys.stdout.flush()

@@ -71,3 +71,29 @@ def test_driver_cmd_branch_spreads_jobs_over_gpus(tmp_path, monkeypatch, nj, ngp
         assert "--device_rr=%d,%d" % (n, ngpu) in argv
         devices.append(_resolve(argv))
     assert devices == [(n - 1) % ngpu for n in range(1, nj + 1)]
+
+
+def test_native_cli_process_never_imports_torch(tmp_path):
+    """A cold compute-fdlp-feats JOB on the native runner (the default) loads libfdlp_hip.so without
+    importing torch (about 2 s per process): whatever happens on this host (no GPU here: the JOB fails at
+    HIP initialisation; on a GPU box it completes), torch is never imported."""
+    import sys
+    import numpy as np
+    from scipy.io import wavfile
+    w = str(tmp_path / "a.wav")
+    wavfile.write(w, 16000, (np.random.default_rng(0).standard_normal(32000) * 1000).astype(np.int16))
+    scp = tmp_path / "w.scp"
+    scp.write_text("u1 %s\n" % w)
+    code = ("import sys\n"
+            "sys.path.insert(0, %r)\n"
+            "from speech_recognition_tools_amd.featgen.computeFDLPSpectrogram import main\n"
+            "try:\n"
+            "    main([%r, %r, '--nfilters=80', '--order=150', '--coeff_num=100', '--coeff_range=0,100',\n"
+            "          '--fduration=1.5', '--fbank_type=cochlear,1,1,1,2.5,1', '--seed=1'])\n"
+            "    print('RESULT ok')\n"
+            "except Exception as e:\n"
+            "    print('RESULT', type(e).__name__)\n"
+            "print('TORCH', 'torch' in sys.modules)\n") % (ROOT, str(scp), str(tmp_path / "o"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert "TORCH False" in r.stdout, r.stdout + r.stderr
+    assert "RESULT" in r.stdout, r.stdout + r.stderr
