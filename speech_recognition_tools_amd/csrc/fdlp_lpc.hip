@@ -248,25 +248,121 @@ __device__ __forceinline__ void cep_fma16(double& a0, double& a1, double& a2, do
   fmac_bcast<15>(a3, kc, v[15]);
 }
 
-// The window blocks w = WI .. W-1 of one cepstrum block (CB < 0): block w's 16 alpha values were issued
-// before this call (va); block w + 1's are issued before block w's FMAs (double buffer), and the wait
-// before the FMAs leaves those 16 in flight (LDS operations complete in order).
-template <int W, int WI>
-__device__ __forceinline__ void cep_window(double& a0, double& a1, double& a2, double& a3, const double (&kc)[W],
-                                           double (&va)[16], double (&vb)[16], uint32_t addr) {
-  if constexpr (WI < W) {
-    if constexpr (WI + 1 < W) {
-      lds_load16<16 * (WI + 1) + 15>(vb, addr);
-      lgkm_wait<15>();  // all of block WI's loads (and the first of WI + 1's) have landed
+// ---- super-block cepstrum (CB < 0: any M, REVERB's 450) -----------------------------------------
+// With d_n = n c_n the recursion of features.py:233-246 (alpha = -a) reads
+//     d_n = -n a_n - sum_{1 <= k < n} d_k a_{n-k},      c_n = d_n / n  (n >= 1),  c_0 = log(sqrt(gg)).
+// Blocks of 16 coefficients, lane l of the item's DPP row owning n = 16 b + l.  For lane l the vector
+//     V_q[j] = a_{16 (q+1) + l - j}   (j < 16)
+// multiplies the 16 d values of a finished block that lies q blocks behind the block being computed, and
+// it does not depend on which block that is.  So a super-block of R consecutive blocks loads each V_q
+// once and uses it for every block r of it (window block w = q - r): 4x fewer LDS reads than one window
+// per block.  The in-block part is the unit lower-triangular Toeplitz system (I + T) d = y, T built from
+// a_1 .. a_15; it is solved as d = H y, H = (I + T)^-1 = the lower Toeplitz matrix of h = the first 16
+// terms of the impulse response of 1/a(z), computed once per item: 16 independent FMAs per block instead
+// of a 16-step serial recurrence.
+
+// acc[r] += kc[Q - r] (.) V_Q for the blocks r of the super-block whose window reaches V_Q (0 <= Q - r < W)
+template <int W, int R, int Q, int J, int Rr>
+__device__ __forceinline__ void sb_fma_r(double (&acc)[R][2], const double (&kc)[W], double v) {
+  if constexpr (Rr < R) {
+    if constexpr (Q - Rr >= 0 && Q - Rr < W) fmac_bcast<J>(acc[Rr][J & 1], kc[Q - Rr], v);
+    sb_fma_r<W, R, Q, J, Rr + 1>(acc, kc, v);
+  }
+}
+template <int W, int R, int Q, int J = 0>
+__device__ __forceinline__ void sb_fma_q(double (&acc)[R][2], const double (&kc)[W], const double (&v)[16]) {
+  if constexpr (J < 16) {
+    sb_fma_r<W, R, Q, J, 0>(acc, kc, v[J]);
+    sb_fma_q<W, R, Q, J + 1>(acc, kc, v);
+  }
+}
+
+// The window phase of one super-block, V_Q .. V_{qmax-1}: V_Q was issued before this call (va), V_{Q+1}
+// is issued before V_Q's FMAs (double buffer; the counted wait leaves those 16 in flight, LDS operations
+// complete in order).  qmax (uniform) = the window blocks that reach a finished block (Q - r < s).
+template <int W, int R, int Q>
+__device__ __forceinline__ void sb_window(double (&acc)[R][2], const double (&kc)[W], double (&va)[16],
+                                          double (&vb)[16], uint32_t addr, int qmax) {
+  if constexpr (Q < W) {
+    if (Q >= qmax) return;
+    if constexpr (Q + 1 < W) {
+      if (Q + 1 < qmax) {
+        lds_load16<16 * (Q + 1) + 15>(vb, addr);
+        lgkm_wait<15>();  // V_Q's 16 loads (and the first of V_{Q+1}'s) have landed (lgkmcnt holds <= 15)
+      } else {
+        lgkm_wait<0>();
+      }
     } else {
       lgkm_wait<0>();
     }
     // the asm loads' results look ready to the compiler: tie them to the wait (a volatile asm that
     // "rewrites" them), so neither the FMAs nor a register copy can be scheduled above it
 #pragma unroll
-    for (int q = 0; q < 16; ++q) asm volatile("" : "+v"(va[q]));
-    cep_fma16(a0, a1, a2, a3, kc[WI], va);
-    cep_window<W, WI + 1>(a0, a1, a2, a3, kc, vb, va, addr);
+    for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(va[j]));
+    sb_fma_q<W, R, Q>(acc, kc, va);
+    sb_window<W, R, Q + 1>(acc, kc, vb, va, addr, qmax);
+  }
+}
+
+// acc += kcnew[T0 - t] (.) V_t, t = 0 .. T0: the blocks of the current super-block before block T0 + 1
+template <int R, int T0, int T = 0>
+__device__ __forceinline__ void sb_local(double (&acc)[2], const double (&kcnew)[R], double (&va)[16],
+                                         double (&vb)[16], uint32_t addr) {
+  if constexpr (T <= T0) {
+    if constexpr (T < T0) {
+      lds_load16<16 * (T + 1) + 15>(vb, addr);
+      lgkm_wait<15>();
+    } else {
+      lgkm_wait<0>();
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(va[j]));
+    cep_fma16(acc[0], acc[1], acc[0], acc[1], kcnew[T0 - T], va);
+    sb_local<R, T0, T + 1>(acc, kcnew, vb, va, addr);
+  }
+}
+
+// d = H y for the block: lane l gets sum_m h_{l-m} y_m (y_m from lane m, Hrow[m] = h_{l-m}, 0 for m > l)
+__device__ __forceinline__ double sb_solve(double y, const double (&Hrow)[16]) {
+  double ym;
+  asm volatile("v_mov_b64 %0, %1\n\ts_nop 1" : "=v"(ym) : "v"(y));  // DPP source: 2 wait states past its write
+  double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
+  fmac_bcast<0>(d0, ym, Hrow[0]);
+  fmac_bcast<1>(d1, ym, Hrow[1]);
+  fmac_bcast<2>(d2, ym, Hrow[2]);
+  fmac_bcast<3>(d3, ym, Hrow[3]);
+  fmac_bcast<4>(d0, ym, Hrow[4]);
+  fmac_bcast<5>(d1, ym, Hrow[5]);
+  fmac_bcast<6>(d2, ym, Hrow[6]);
+  fmac_bcast<7>(d3, ym, Hrow[7]);
+  fmac_bcast<8>(d0, ym, Hrow[8]);
+  fmac_bcast<9>(d1, ym, Hrow[9]);
+  fmac_bcast<10>(d2, ym, Hrow[10]);
+  fmac_bcast<11>(d3, ym, Hrow[11]);
+  fmac_bcast<12>(d0, ym, Hrow[12]);
+  fmac_bcast<13>(d1, ym, Hrow[13]);
+  fmac_bcast<14>(d2, ym, Hrow[14]);
+  fmac_bcast<15>(d3, ym, Hrow[15]);
+  return (d0 + d1) + (d2 + d3);
+}
+
+// Hrow[m] = h_{l-m} (0 for m > l) from hl = h_l: DPP row_shr:m with bound_ctrl (lanes l < m take 0)
+template <int M0 = 1>
+__device__ __forceinline__ void sb_hrow(double (&Hrow)[16], double hl) {
+  if constexpr (M0 < 16) {
+    Hrow[M0] = __builtin_amdgcn_update_dpp(0.0, hl, 0x110 + M0, 0xF, 0xF, true);
+    sb_hrow<M0 + 1>(Hrow, hl);
+  }
+}
+
+// h_1 .. h_15 of 1/a(z) (h_0 = 1, h_m = -sum_{k=1}^{m} a_k h_{m-k}): lane l ends with h_l
+template <int M0 = 1>
+__device__ __forceinline__ void sb_impulse(double& hl, double& t, const double* la, int l) {
+  if constexpr (M0 < 16) {
+    if (l == M0) hl = -t;
+    const double hm = dpp_f64<0x150 + M0>(hl);  // row_newbcast:M0
+    if (l > M0) t = fma(hm, la[l - M0], t);
+    sb_impulse<M0 + 1>(hl, t, la, l);
   }
 }
 
@@ -573,11 +669,15 @@ constexpr int kEnvChunk = 5;  // envelope slots held in registers at a time
 // DM: the Durbin phase.  1: the contiguous-chunk Durbin (contig_durbin, p outside durbin8_kernel's
 // range); 2: none, a and gg come from durbin8_kernel (A.a_ext, A.gg_ext; default where it is instantiated).
 constexpr int kDmContig = 1, kDmExt = 2;
-template <int SL, int CB = 0, int DM = kDmContig>
 #ifndef FDLP_LAT_WAVES
 #define FDLP_LAT_WAVES 4  // waves per SIMD the lattice kernel is compiled for (register budget)
 #endif
-__global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(LpcEnvArgs A_) {
+// the super-block cepstrum (CB < 0) holds ~70 doubles of window, H rows and accumulators (spills at 3
+// waves per SIMD); its LDS allows 2.5 per SIMD anyway
+template <int CB>
+constexpr int lat_waves() { return CB < 0 ? 2 : FDLP_LAT_WAVES; }
+template <int SL, int CB = 0, int DM = kDmContig>
+__global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(LpcEnvArgs A_) {
   extern __shared__ double sh[];
   const LpcEnvArgs& A = A_;
   const int ngroups = (A.items + 3) >> 2;
@@ -686,37 +786,59 @@ __global__ __launch_bounds__(64, FDLP_LAT_WAVES) void lpc_env_lattice_kernel(Lpc
       }
       wave_lds_sync();
     } else if constexpr (CB < 0) {
-      // any M (REVERB: 450): the same register broadcast over a sliding window of the last W finished
-      // blocks.  alpha_{n-k} = 0 for n - k > p, and the window covers every k >= b0 - 16 W <= n - p, so
-      // the terms it adds beyond the reference's range are exact zeros (la is zero past p).
-      constexpr int W = SL;  // block w holds n - k >= 16 w + 1; w >= ceil(p / 16) <= SL is all zero terms
-      double kc[W];              // kc[w]: n c_n (lane l) of block b - 1 - w; 0 before block 0
+      // any M (REVERB: 450): super-blocks of R blocks (see sb_window above).  alpha_{n-k} = 0 for n - k > p,
+      // and V_q, q < W = SL, covers every lag up to 16 SL + 15 >= p + 15, so the terms added beyond the
+      // reference's range are exact zeros (la is zero from p + 1 to la_len).
+      constexpr int W = SL;
+      constexpr int R = 4;
+      double kc[W];  // kc[w]: d (lane l) of block s - 1 - w of the current super-block s; 0 before block 0
 #pragma unroll
       for (int w = 0; w < W; ++w) kc[w] = 0.0;
+      // h and the H rows of this item (a_1 .. a_15 from la)
+      double Hrow[16];
+      {
+        double t = l >= 1 ? la[l] : 0.0;  // sum_{i < l} h_i a_{l-i}, so far i = 0
+        double hl = l == 0 ? 1.0 : 0.0;
+        sb_impulse<1>(hl, t, la, l);
+        Hrow[0] = hl;
+        sb_hrow<1>(Hrow, hl);
+      }
       // only c_0 .. c_{Me-1} reach the envelope (fft(., env_nfft) truncates, :201); all M are computed
       // when the cepstra themselves are an output (debug / modulation-spectrum mode)
       const int Mc = A.cep_out ? M : A.Me;
-      for (int b0 = 0; b0 < ((FDLP_LPC_PHASES & 2) ? Mc : 0); b0 += 16) {
-        const int n = b0 + l;
-        const double inv_n = 1.0 / (double)(n > 0 ? n : 1);
-        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-        asm volatile("s_nop 1");  // kc[0] was just written: DPP reads need 2 wait states
-        // k = b0 - 16 (w + 1) + j: alpha_{n-k} = la[n - b0 + 16 w + 16 - j]; the lane's base address is
-        // la + n - b0 + 1, so window block w reads byte offsets 8 (16 w + 15 - j)
-        double va[16], vb[16];
-        const uint32_t aaddr =
-            (uint32_t)(uintptr_t)((__attribute__((address_space(3))) double*)(la + n - b0 + 1));
-        lgkm_wait<0>();  // nothing else (scalar loads complete out of order) may share the counted waits
-        lds_load16<15>(va, aaddr);
-        cep_window<W, 0>(a0, a1, a2, a3, kc, va, vb, aaddr);
-        double acc = (a0 + a1) + (a2 + a3);
-        double mine = 0.0;
-        cep_block_step<0>(b0, Mc, l, gg, inv_n, la, n, acc, mine, p);
+      const int NB = (FDLP_LPC_PHASES & 2) ? (Mc + 15) >> 4 : 0;
+      // the lane's LDS byte address la + l + 1: V_q[j] = la[16 (q+1) + l - j] at byte offset 8 (16 q + 15 - j)
+      const uint32_t aaddr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) double*)(la + l + 1));
+      for (int sb = 0; sb < NB; sb += R) {
+        double acc[R][2];
 #pragma unroll
-        for (int w = W - 1; w > 0; --w) kc[w] = kc[w - 1];
-        kc[0] = n == 0 ? 0.0 : (double)n * mine;
-        if (n < CSN) cs[n] = mine;
-        if (n < M && valid && A.cep_out) A.cep_out[(int64_t)item * M + n] = mine;
+        for (int r = 0; r < R; ++r) acc[r][0] = acc[r][1] = 0.0;
+        double va[16], vb[16];
+        const int qmax = min(W, sb + R - 1);  // V_q reaches a finished block (q - r < sb) for some r
+        asm volatile("s_nop 1");  // kc was just written: DPP reads need 2 wait states
+        lgkm_wait<0>();  // nothing else (scalar loads complete out of order) may share the counted waits
+        if (qmax > 0) {
+          lds_load16<15>(va, aaddr);
+          sb_window<W, R, 0>(acc, kc, va, vb, aaddr, qmax);
+        }
+        double kcnew[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int n = 16 * (sb + r) + l;
+          if (r == 1) { lds_load16<15>(va, aaddr); sb_local<R, 0>(acc[1], kcnew, va, vb, aaddr); }
+          if (r == 2) { lds_load16<15>(va, aaddr); sb_local<R, 1>(acc[2], kcnew, va, vb, aaddr); }
+          if (r == 3) { lds_load16<15>(va, aaddr); sb_local<R, 2>(acc[3], kcnew, va, vb, aaddr); }
+          const double an = n <= p ? la[min(n, p)] : 0.0;
+          const double y = -(double)n * an - (acc[r][0] + acc[r][1]);
+          const double d = sb_solve(y, Hrow);
+          kcnew[r] = d;
+          const double c = n == 0 ? log(sqrt(gg)) : d * (1.0 / (double)(n > 0 ? n : 1));
+          if (n < CSN) cs[n] = c;
+          if (n < M && valid && A.cep_out) A.cep_out[(int64_t)item * M + n] = c;
+          asm volatile("s_nop 1");  // kcnew[r] feeds the next block's DPP-broadcast FMAs
+        }
+#pragma unroll
+        for (int w = W - 1; w >= 0; --w) kc[w] = w >= R ? kc[w - R] : kcnew[R - 1 - w];
       }
       wave_lds_sync();
     }
