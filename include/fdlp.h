@@ -110,6 +110,9 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out);
 int fdlp_plan_destroy(fdlp_plan* plan);
 const char* fdlp_last_error(void);
 int fdlp_abi_version(void);
+/* Device address of pinned host memory (hipHostMalloc / hipHostRegister): fdlp_batch.out_dev may point
+ * there, the OLA kernel then stores the features straight into host memory (no D2H copy; ABI 4). */
+int fdlp_mapped_ptr(void* host, void** dev);
 
 /* Frame geometry of one utterance of T samples: F analysis frames (getFrames,
  * features.py:151) and L output frames (int(ceil(T*frate/srate)), :182; L = F for the modspec

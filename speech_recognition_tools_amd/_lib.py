@@ -113,6 +113,7 @@ SIGNATURES = {
     "fdlp_plan_destroy": (c_i32, [c_p]),
     "fdlp_last_error": (ctypes.c_char_p, []),
     "fdlp_abi_version": (c_i32, []),
+    "fdlp_mapped_ptr": (c_i32, [c_p, ctypes.POINTER(c_p)]),
     "fdlp_geometry": (c_i32, [c_p, c_i64, P_i32, P_i32]),
     "fdlp_plan_info": (c_i32, [c_p, P_i32, P_i32, P_i32, P_i32, P_i32]),
     "fdlp_plan_out_dim": (c_i32, [c_p, P_i32]),

@@ -193,47 +193,6 @@ __global__ __launch_bounds__(256) void dft2_dct_kernel(DevConsts c, DftPlan d2, 
 // (rows) per workgroup, and a branch-free sample gather for frames that need no reflect padding.
 // Same arithmetic order per butterfly as the generic passes (Stockham DIT, twiddle then DFT).
 // -----------------------------------------------------------------------------------------
-template <int R>
-__device__ __forceinline__ void bfly_c(double2 (&v)[R]) {
-  if constexpr (R == 2) {
-    const double2 a = v[0], b = v[1];
-    v[0] = cadd(a, b);
-    v[1] = make_double2(a.x - b.x, a.y - b.y);
-  } else if constexpr (R == 4) {
-    const double2 a0 = cadd(v[0], v[2]), a1 = make_double2(v[0].x - v[2].x, v[0].y - v[2].y);
-    const double2 b0 = cadd(v[1], v[3]), b1 = make_double2(v[1].x - v[3].x, v[1].y - v[3].y);
-    const double2 b1m = make_double2(b1.y, -b1.x);  // -i b1
-    v[0] = cadd(a0, b0);
-    v[2] = make_double2(a0.x - b0.x, a0.y - b0.y);
-    v[1] = cadd(a1, b1m);
-    v[3] = make_double2(a1.x - b1m.x, a1.y - b1m.y);
-  } else if constexpr (R == 3) {
-    constexpr double c1 = -0.5, s1 = -0.86602540378443864676;  // e^{-2 pi i / 3}
-    const double2 t = cadd(v[1], v[2]);
-    const double2 d = make_double2(v[1].x - v[2].x, v[1].y - v[2].y);
-    const double2 m = make_double2(v[0].x + c1 * t.x, v[0].y + c1 * t.y);
-    const double2 u = make_double2(-s1 * d.y, s1 * d.x);  // i s1 d
-    v[0] = cadd(v[0], t);
-    v[1] = cadd(m, u);
-    v[2] = make_double2(m.x - u.x, m.y - u.y);
-  } else if constexpr (R == 5) {
-    constexpr double c1 = 0.30901699437494742410, s1 = -0.95105651629515357212;  // e^{-2 pi i / 5}
-    constexpr double c2 = -0.80901699437494742410, s2 = -0.58778525229247312917; // e^{-4 pi i / 5}
-    const double2 t1 = cadd(v[1], v[4]), d1 = make_double2(v[1].x - v[4].x, v[1].y - v[4].y);
-    const double2 t2 = cadd(v[2], v[3]), d2 = make_double2(v[2].x - v[3].x, v[2].y - v[3].y);
-    const double2 m1 = make_double2(v[0].x + c1 * t1.x + c2 * t2.x, v[0].y + c1 * t1.y + c2 * t2.y);
-    const double2 m2 = make_double2(v[0].x + c2 * t1.x + c1 * t2.x, v[0].y + c2 * t1.y + c1 * t2.y);
-    // i (s1 d1 + s2 d2) and i (s2 d1 - s1 d2)
-    const double2 u1 = make_double2(-(s1 * d1.y + s2 * d2.y), s1 * d1.x + s2 * d2.x);
-    const double2 u2 = make_double2(-(s2 * d1.y - s1 * d2.y), s2 * d1.x - s1 * d2.x);
-    v[0] = cadd(cadd(v[0], t1), t2);
-    v[1] = cadd(m1, u1);
-    v[4] = make_double2(m1.x - u1.x, m1.y - u1.y);
-    v[2] = cadd(m2, u2);
-    v[3] = make_double2(m2.x - u2.x, m2.y - u2.y);
-  }
-}
-
 // LDS slot of element (pos, col) of COLS = 8 interleaved columns.  SWZ: the column index XORed with
 // g(pos mod 8) = ((pos & 1) << 2) | ((pos & 7) >> 1), so 8 consecutive positions of one column (the
 // row pass's coalesced load order) land in 8 different 16-byte bank groups, while the 8 columns of one

@@ -648,8 +648,15 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     copies.wait(slot_i);  // every utterance of the batch is in the pinned buffer
     int r = grow_device(&sl.d_pcm, &sl.d_pcm_cap, (size_t)pend.samples * elem, s);
     if (r != FDLP_OK) return r;
-    r = grow_device((void**)&sl.d_out, &sl.out_cap, sizeof(float) * (size_t)pend.out_rows * B, s);
-    if (r != FDLP_OK) return r;
+    // features: the OLA kernel stores them straight into the slot's pinned host buffer (mapped into the
+    // device address space), so no D2H copy, no blit kernel competing for CUs; with --cmvn_stats they stay
+    // in device memory for the statistics kernel and are copied out
+    float* h_out_dev = nullptr;
+    if (!d_cmvn && hipHostGetDevicePointer((void**)&h_out_dev, sl.h_out, 0) != hipSuccess) h_out_dev = nullptr;
+    if (!h_out_dev) {
+      r = grow_device((void**)&sl.d_out, &sl.out_cap, sizeof(float) * (size_t)pend.out_rows * B, s);
+      if (r != FDLP_OK) return r;
+    }
     // copy-in on its own stream so it overlaps the previous batch's kernels
     if (hipMemcpyAsync(sl.d_pcm, sl.h_pcm, (size_t)pend.samples * elem, hipMemcpyHostToDevice, s_in) != hipSuccess ||
         hipEventRecord(sl.ev_in, s_in) != hipSuccess || hipStreamWaitEvent(s, sl.ev_in, 0) != hipSuccess)
@@ -664,7 +671,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     b.noise_dev = o->noise ? d_noise : nullptr;
     b.noise_off = o->noise ? pend.noff.data() : nullptr;
     b.noise_alpha = o->noise ? pend.alpha.data() : nullptr;
-    b.out_dev = sl.d_out;
+    b.out_dev = h_out_dev ? h_out_dev : sl.d_out;
     b.out_row = pend.rows.data();
     b.out_f64_dev = nullptr;
     b.ark_decimals = o->ark_decimals;
@@ -675,12 +682,14 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
       r = fdlp_cmvn_accumulate(sl.d_out, pend.out_rows, B, d_cmvn, s);
       if (r != FDLP_OK) return r;
     }
-    // copy-out on its own stream so it overlaps the next batch's kernels
-    if (hipEventRecord(sl.ev_comp, s) != hipSuccess || hipStreamWaitEvent(s_out, sl.ev_comp, 0) != hipSuccess ||
-        hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * (size_t)pend.out_rows * B, hipMemcpyDeviceToHost, s_out) !=
-            hipSuccess ||
-        hipEventRecord(sl.done, s_out) != hipSuccess)
+    if (h_out_dev) {  // the features are in h_out once the compute stream passes this point
+      if (hipEventRecord(sl.done, s) != hipSuccess) return fail(FDLP_E_HIP, "event record failed");
+    } else if (hipEventRecord(sl.ev_comp, s) != hipSuccess || hipStreamWaitEvent(s_out, sl.ev_comp, 0) != hipSuccess ||
+               hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * (size_t)pend.out_rows * B, hipMemcpyDeviceToHost,
+                              s_out) != hipSuccess ||
+               hipEventRecord(sl.done, s_out) != hipSuccess) {  // copy-out on its own stream (overlaps the next batch)
       return fail(FDLP_E_HIP, "D2H copy failed");
+    }
     Done d;
     d.slot = slot_i;
     d.ids = std::move(pend.ids);
@@ -704,7 +713,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     for (size_t k = 0; k < slots.size(); ++k) {
       Slot& sl = slots[k];
       JOB_TRY(grow_device(&sl.d_pcm, &sl.d_pcm_cap, smp * sizeof(int16_t), s));
-      JOB_TRY(grow_device((void**)&sl.d_out, &sl.out_cap, rows * B * sizeof(float), s));
+      if (o->cmvn_path) JOB_TRY(grow_device((void**)&sl.d_out, &sl.out_cap, rows * B * sizeof(float), s));
     }
   }
 

@@ -248,6 +248,73 @@ __device__ __forceinline__ void cep_fma16(double& a0, double& a1, double& a2, do
   fmac_bcast<15>(a3, kc, v[15]);
 }
 
+// ---- FFT envelope (env_nfft = 300 with Me = 300: REVERB) -----------------------------------------
+// Re(fft(c', 300))[t] (computeFDLPSpectrogram.py:201-205, scipy's own FFT route) from a 150-point complex
+// FFT of z[q] = c'_{2q} + i c'_{2q+1} -- the weighted cepstrum buffer read as double2, so no packing --
+// then the real-FFT unpacking Re X_t = (Z_t + conj Z_{-t}).x / 2 + Re(w^t (Z_t - conj Z_{-t}) / 2i),
+// w = e^{-2 pi i / 300}.  One 16-lane row per item, Stockham stages in place in LDS (all butterflies of
+// a stage read into registers, then written back; the row's LDS ops complete in order).  ~0.4k
+// instructions per lane and item instead of the ~3k FMAs of the direct cosine sum.  Roots from the
+// plan's cos(2 pi q / 300) table: w_150^e = cos(2 pi 2e/300) - i sin(.), sin x = cos(x - pi/2).
+template <int N, int R, int Ns>
+__device__ __forceinline__ void env_fft_stage(double2* buf, const double* __restrict__ cosT, int l) {
+  constexpr int NB = N / R, IT = (NB + 15) / 16, TW0 = N / (Ns * R);
+  double2 v[IT][R];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int j = l + 16 * it;
+    if (j < NB) {
+      const int k = j % Ns;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const double2 x = buf[j + r * NB];
+        if (r == 0 || Ns == 1) {
+          v[it][r] = x;
+        } else {
+          const int e2 = 2 * TW0 * k * r;  // < 300
+          const double2 w = make_double2(cosT[e2], -cosT[e2 >= 75 ? e2 - 75 : e2 + 225]);
+          v[it][r] = cmul(x, w);
+        }
+      }
+      bfly_c<R>(v[it]);
+    }
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int j = l + 16 * it;
+    if (j < NB) {
+      const int k = j % Ns, jq = j / Ns;
+      const int idxD = jq * Ns * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) buf[idxD + r * Ns] = v[it][r];
+    }
+  }
+  wave_lds_sync();
+}
+
+// env[t] = exp(Re X_t) * hann/hamm[t], t < 150, from the weighted cepstrum cw[0 .. 300) (16-B aligned)
+__device__ __forceinline__ void env_fft300(double* cw, const double* __restrict__ cosT,
+                                           const double* __restrict__ win, double* out, int l, bool valid) {
+  double2* z = reinterpret_cast<double2*>(cw);
+  env_fft_stage<150, 2, 1>(z, cosT, l);
+  env_fft_stage<150, 3, 2>(z, cosT, l);
+  env_fft_stage<150, 5, 6>(z, cosT, l);
+  env_fft_stage<150, 5, 30>(z, cosT, l);
+  if (!valid) return;
+#pragma unroll
+  for (int it = 0; it < 10; ++it) {
+    const int t = l + 16 * it;
+    if (t < 150) {
+      const int m = t == 0 ? 0 : 150 - t;
+      const double2 Zt = z[t], Zm = z[m];
+      const double c = cosT[t], s = cosT[t >= 75 ? t - 75 : t + 225];
+      const double re = 0.5 * (Zt.x + Zm.x) + 0.5 * (c * (Zt.y + Zm.y) - s * (Zt.x - Zm.x));
+      out[t] = exp(re) * win[2 * t];
+    }
+  }
+}
+
 // ---- super-block cepstrum (CB < 0: any M, REVERB's 450) -----------------------------------------
 // With d_n = n c_n the recursion of features.py:233-246 (alpha = -a) reads
 //     d_n = -n a_n - sum_{1 <= k < n} d_k a_{n-k},      c_n = d_n / n  (n >= 1),  c_0 = log(sqrt(gg)).
@@ -881,6 +948,12 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
       cw[n] = v;
     }
     wave_lds_sync();
+    if constexpr (CB < 0) {
+      if (A.env_nfft == 300 && A.Me == 300 && A.kk == 150) {  // the recipes' REVERB envelope: FFT route
+        if (FDLP_LPC_PHASES & 4) env_fft300(cw, A.env_cos, A.env_win, A.env + (int64_t)(valid ? item : 0) * A.kk, l, valid);
+        continue;
+      }
+    }
     // S(u) = Even(u) + Odd(u), S(H - u) = Even(u) - Odd(u); lane slots cover u = 0..H/2 (lpc_env_kernel)
     for (int q0 = 0; q0 < TS; q0 += kEnvChunk) {
       double se[kEnvChunk], so[kEnvChunk], cprev[kEnvChunk], ccur[kEnvChunk], c2[kEnvChunk];

@@ -486,6 +486,13 @@ extern "C" {
 const char* fdlp_last_error(void) { return fdlp::last_error_slot().c_str(); }
 int fdlp_abi_version(void) { return FDLP_ABI_VERSION; }
 
+int fdlp_mapped_ptr(void* host, void** dev) {
+  if (!host || !dev) return fail(FDLP_E_INVALID, "fdlp_mapped_ptr: bad args");
+  if (hipHostGetDevicePointer(dev, host, 0) != hipSuccess)
+    return fail(FDLP_E_INVALID, "fdlp_mapped_ptr: not pinned host memory (hipHostMalloc / hipHostRegister)");
+  return FDLP_OK;
+}
+
 int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   if (!cfg || !out) return fail(FDLP_E_INVALID, "fdlp_plan_create: null argument");
   *out = nullptr;

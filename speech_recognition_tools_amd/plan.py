@@ -121,7 +121,7 @@ class FdlpPlan:
         D = self.out_dim
         if out is None:
             out = torch.empty((total, D), dtype=torch.float32, device=dev)
-        elif out.shape[0] < total or out.shape[1] != D or out.dtype != torch.float32:
+        elif out.shape[0] < total or out.shape[1] != D or out.dtype != torch.float32 or not out.is_contiguous():
             raise ValueError("out buffer too small")
         out64 = torch.empty((total, D), dtype=torch.float64, device=dev) if want_f64 else None
         jit = np.ascontiguousarray(np.zeros(1) if jitter is None else jitter, dtype=np.uint8)
@@ -136,7 +136,14 @@ class FdlpPlan:
             na = np.ascontiguousarray(np.asarray(noise_alpha, dtype=np.float64))
             keep += [no, na]
             b.noise_dev, b.noise_off, b.noise_alpha = noise.data_ptr(), ptr(no, ctypes.c_int64), ptr(na, ctypes.c_double)
-        b.out_dev = out.data_ptr()
+        if out.is_cuda:
+            b.out_dev = out.data_ptr()
+        elif out.is_pinned():  # the OLA kernel stores into pinned host memory through its device mapping
+            dp = ctypes.c_void_p()
+            check(lib.fdlp_mapped_ptr(ctypes.c_void_p(out.data_ptr()), ctypes.byref(dp)))
+            b.out_dev = dp.value
+        else:
+            raise ValueError("out must be a device tensor or a pinned host tensor")
         rows_c = np.ascontiguousarray(rows[:-1])
         b.out_row = ptr(rows_c, ctypes.c_int64)
         b.out_f64_dev = out64.data_ptr() if out64 is not None else None

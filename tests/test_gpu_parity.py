@@ -336,3 +336,24 @@ def test_batches_in_flight_on_streams_match_serial():
     torch.cuda.synchronize()
     for k in range(3):
         np.testing.assert_array_equal(res[k].cpu().numpy(), ref[k])
+
+
+def test_features_into_pinned_host_memory_match_device_output():
+    """fdlp_compute with out_dev = the device mapping of a pinned host buffer (fdlp_mapped_ptr: the OLA
+    kernel stores the features straight into host memory, the JOB runner's and bench's PCIe path) gives
+    bit-identical features to a device output buffer."""
+    from speech_recognition_tools_amd import FdlpPlan, PyRandom
+    meta, sig, ref, z = load_golden("wsj")
+    plan = FdlpPlan(feature_cfg(meta), device=0, max_frames=256)
+    utts = meta["utts"]
+    lens = [sig[u].size for u in utts]
+    pcm = torch.from_numpy(np.concatenate([sig[u] for u in utts])).cuda()
+    nj = sum(max(plan.geometry(int(T))[0] - 1, 0) for T in lens)
+    jit = PyRandom(meta["seed"]).randbits2(nj)
+    dev_out, rows, _ = plan.compute(pcm, lens, jit)
+    host = torch.full(tuple(dev_out.shape), float("nan"), dtype=torch.float32).pin_memory()
+    plan.compute(pcm, lens, jit, out=host)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(host.numpy(), dev_out.cpu().numpy())
+    with pytest.raises(ValueError):
+        plan.compute(pcm, lens, jit, out=torch.empty(tuple(dev_out.shape), dtype=torch.float32))
