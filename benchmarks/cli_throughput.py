@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--workers", type=int, nargs="+", default=[1, 4, 8])
     ap.add_argument("--batch-frames", type=int, default=8192)
     ap.add_argument("--profile", default=None, help="write cProfile stats of the last run to this file")
-    ap.add_argument("--runners", nargs="+", default=["native", "python"], choices=["native", "python"])
+    ap.add_argument("--runners", nargs="+", default=["native", "python"], choices=["native", "native_mapped", "python"])
     a = ap.parse_args()
     from bench import speech_like_batch
     from speech_recognition_tools_amd.featgen import computeFDLPSpectrogram as cli
@@ -53,7 +53,8 @@ def main():
         sys.stdout = so
         for runner, w in [(r, w) for r in a.runners for w in a.workers]:
             args = build_parser().parse_args([os.path.join(d, "wav.scp"), os.path.join(d, "o%d" % w),
-                                              "--io_workers=%d" % w, "--host_runner=" + runner] + opts)
+                                              "--io_workers=%d" % w, "--host_runner=" + runner.split("_")[0]] +
+                                             (["--mapped_output"] if runner == "native_mapped" else []) + opts)
             sys.stdout = devnull
             prof = None
             if a.profile:
@@ -76,7 +77,7 @@ def main():
                               "host_runner": runner,
                               "utts": a.utts, "utt_seconds": a.seconds, "seconds": el,
                               "ark_bytes": os.path.getsize(os.path.join(d, "o%d.ark" % w)),
-                              "job_stats": cli.LAST_JOB_STATS if runner == "native" else None}))
+                              "job_stats": cli.LAST_JOB_STATS if runner.startswith("native") else None}))
             sys.stdout.flush()
 
 

@@ -345,6 +345,8 @@ typedef struct fdlp_job_opts {
   int32_t srate;               /* the sample rate the reference asserts (16000, :144)                 */
   const char* progress_name;   /* non-NULL: "<name>: Computing Features for file: <utt>" per utterance */
   const char* cmvn_path;       /* non-NULL: global CMVN stats (Kaldi binary DM) of the written features */
+  int32_t out_mapped;          /* 1: the OLA kernel stores the features straight into the pinned host
+                                  slots (no D2H copy); 0 (default): device buffer + D2H copy (ABI 4)   */
 } fdlp_job_opts;
 typedef struct fdlp_job_stats {
   int64_t n_lines;             /* scp entries                                  */

@@ -94,7 +94,7 @@ class FdlpJobOptsC(ctypes.Structure):
         ("scp_type", c_i32), ("write_len", c_i32), ("ark_decimals", c_i32), ("batch_frames", c_i32),
         ("io_threads", c_i32), ("preprocess", c_i32), ("noise", P_i16), ("noise_len", c_i64), ("snr", c_dbl),
         ("noise_seed", ctypes.c_uint32), ("jitter_key", P_u32), ("jitter_key_len", c_i32), ("srate", c_i32),
-        ("progress_name", ctypes.c_char_p), ("cmvn_path", ctypes.c_char_p),
+        ("progress_name", ctypes.c_char_p), ("cmvn_path", ctypes.c_char_p), ("out_mapped", c_i32),
     ]
 
 

@@ -597,29 +597,6 @@ __device__ __forceinline__ void vs_fma_rows(double (&acc)[A], double cur, const 
     vs_fma_rows<A, V + 1>(acc, cur, lo, hi);
   }
 }
-// The same A^2 FMAs with the window values of the previous block (hi, in registers since the last
-// block) first and the current block's (lo, loaded at the block's start) last: the A(A-1)/2 hi terms
-// cover the LDS latency of the lo loads (the asm FMAs are issued in source order, and the wait for lo
-// lands before the first lo term).  Consecutive FMAs still target different accumulators.
-template <int A, int V = A - 1>
-__device__ __forceinline__ void vs_fma_rows_hi(double (&acc)[A], double cur, const double (&hi)[A]) {
-  if constexpr (V > 0) {
-#pragma unroll
-    for (int u = A - V; u < A; ++u) fmac_bcast<V>(acc[u], cur, hi[V + u - A]);
-    vs_fma_rows_hi<A, V - 1>(acc, cur, hi);
-  }
-}
-template <int A, int V = 0>
-__device__ __forceinline__ void vs_fma_rows_lo(double (&acc)[A], double cur, const double (&lo)[A]) {
-  if constexpr (V < A) {
-#pragma unroll
-    for (int u = 0; u < A - V; ++u) fmac_bcast<V>(acc[u], cur, lo[V + u]);
-    vs_fma_rows_lo<A, V + 1>(acc, cur, lo);
-  }
-}
-#ifndef FDLP_VS_HIFIRST
-#define FDLP_VS_HIFIRST 1
-#endif
 template <int A>
 __device__ __forceinline__ void vs_fma_block(double (&acc)[A], double cur, const double (&lo)[A],
                                              const double (&hi)[A]) {
@@ -635,12 +612,7 @@ __device__ __forceinline__ void vs_fma_block(double (&acc)[A], double cur, const
   // inside the asm): copy it through one asm that ends in the wait
   double cm;
   asm volatile("v_mov_b64 %0, %1\n\ts_nop 1" : "=v"(cm) : "v"(cur));
-  if constexpr (FDLP_VS_HIFIRST != 0) {
-    vs_fma_rows_hi<A>(acc, cm, hi);
-    vs_fma_rows_lo<A>(acc, cm, lo);
-  } else {
-    vs_fma_rows<A>(acc, cm, lo, hi);
-  }
+  vs_fma_rows<A>(acc, cm, lo, hi);
 #endif
 }
 

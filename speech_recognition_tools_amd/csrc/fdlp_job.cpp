@@ -648,11 +648,12 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     copies.wait(slot_i);  // every utterance of the batch is in the pinned buffer
     int r = grow_device(&sl.d_pcm, &sl.d_pcm_cap, (size_t)pend.samples * elem, s);
     if (r != FDLP_OK) return r;
-    // features: the OLA kernel stores them straight into the slot's pinned host buffer (mapped into the
-    // device address space), so no D2H copy, no blit kernel competing for CUs; with --cmvn_stats they stay
-    // in device memory for the statistics kernel and are copied out
+    // out_mapped: the OLA kernel stores the features straight into the slot's pinned host buffer (mapped
+    // into the device address space), no D2H copy; with --cmvn_stats they stay in device memory for the
+    // statistics kernel.  Default: device buffer + D2H copy on the copy-out stream
     float* h_out_dev = nullptr;
-    if (!d_cmvn && hipHostGetDevicePointer((void**)&h_out_dev, sl.h_out, 0) != hipSuccess) h_out_dev = nullptr;
+    if (o->out_mapped && !d_cmvn && hipHostGetDevicePointer((void**)&h_out_dev, sl.h_out, 0) != hipSuccess)
+      h_out_dev = nullptr;
     if (!h_out_dev) {
       r = grow_device((void**)&sl.d_out, &sl.out_cap, sizeof(float) * (size_t)pend.out_rows * B, s);
       if (r != FDLP_OK) return r;
@@ -713,7 +714,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     for (size_t k = 0; k < slots.size(); ++k) {
       Slot& sl = slots[k];
       JOB_TRY(grow_device(&sl.d_pcm, &sl.d_pcm_cap, smp * sizeof(int16_t), s));
-      if (o->cmvn_path) JOB_TRY(grow_device((void**)&sl.d_out, &sl.out_cap, rows * B * sizeof(float), s));
+      if (!o->out_mapped || o->cmvn_path) JOB_TRY(grow_device((void**)&sl.d_out, &sl.out_cap, rows * B * sizeof(float), s));
     }
   }
 

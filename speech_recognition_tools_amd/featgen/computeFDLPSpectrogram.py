@@ -56,6 +56,9 @@ def build_parser():
                         help='"JOB,N": run on device (JOB-1) mod N (what make_FDLPspectrum_feats.sh --ngpu N '
                              'passes, so Kaldi $cmd array jobs spread over the GPUs)')
     parser.add_argument('--batch_frames', type=int, default=2048, help='analysis frames per GPU batch')
+    parser.add_argument('--mapped_output', action='store_true',
+                        help='native runner: the features go from the kernel straight into pinned host memory '
+                             '(no D2H copy)')
     parser.add_argument('--ark_precision', type=int, default=3,
                         help="decimals of the reference's text ark ('%%.3f'); -1 keeps full float32")
     parser.add_argument('--support_eps', type=float, default=None,
@@ -310,6 +313,7 @@ def _run_native(args, cfg, device, noise, snr, diff):
     # the reference's progress lines, from the C runtime's stdout (only when Python's stdout is the process's)
     o.progress_name = sys.argv[0].encode() if sys.stdout is sys.__stdout__ else None
     o.cmvn_path = args.cmvn_stats.encode() if args.cmvn_stats else None
+    o.out_mapped = int(bool(getattr(args, 'mapped_output', False)))
     st = _lib.FdlpJobStatsC()
     sys.stdout.flush()
     rc = _lib.lib.fdlp_job_run(ctypes.byref(c), int(device), args.scp.encode(), args.outfile.encode(),
