@@ -30,7 +30,8 @@ sys.path.insert(0, ROOT)
 
 WSJ_OPTS = ["--nfilters", "80", "--order", "150", "--fduration", "1.5", "--frate", "100", "--coeff_num", "100",
             "--coeff_range", "0,100", "--overlap_fraction", "0.25", "--fbank_type", "cochlear,1,1,1,2.5,1",
-            "--write_utt2num_frames", "true"]  # e2e/wsj/run_fdlp_e1.sh:54-95
+            "--write_utt2num_frames", "true",  # e2e/wsj/run_fdlp_e1.sh:54-95
+            "--add_opts", "--job_stats"]       # per-JOB phase timings into the JOB logs
 
 
 def main():
@@ -71,11 +72,13 @@ def main():
             sys.exit(r.returncode)
         n_feats = sum(1 for _ in open(os.path.join(data, "feats.scp")))
         frames = sum(int(l.split()[1]) for l in open(os.path.join(data, "utt2num_frames")))
-        job_s = []
+        job_s, stats = [], []
         for n in range(1, a.nj + 1):
             for line in open(os.path.join(data, "log", "feats_train_si284.%d.log" % n)):
                 if line.startswith("Execution Time:"):
                     job_s.append(float(line.split()[2]))
+                if ": job stats " in line:
+                    stats.append(json.loads(line.split(": job stats ", 1)[1]))
         audio_h = sum(lens) / 16000.0 / 3600.0
         from speech_recognition_tools_amd.shard import visible_gpu_count
         ngpu = a.ngpu or max(1, visible_gpu_count())  # the driver's own rule
@@ -85,6 +88,7 @@ def main():
                           "jobs_per_gpu": a.jobs_per_gpu, "ngpu": ngpu, "feats_scp_lines": n_feats,
                           "frames": frames, "job_execution_s": job_s,
                           "job_execution_s_mean": float(np.mean(job_s)) if job_s else None,
+                          "job_stats_mean": {k: float(np.mean([s[k] for s in stats])) for k in stats[0]} if stats else None,
                           "note": "wall from the driver's start to feats.scp; every JOB is a cold process "
                                   "(interpreter, imports, HIP init, plan build, reads, kernels, writes)"}))
 

@@ -56,6 +56,8 @@ def build_parser():
                         help='"JOB,N": run on device (JOB-1) mod N (what make_FDLPspectrum_feats.sh --ngpu N '
                              'passes, so Kaldi $cmd array jobs spread over the GPUs)')
     parser.add_argument('--batch_frames', type=int, default=2048, help='analysis frames per GPU batch')
+    parser.add_argument('--job_stats', action='store_true',
+                        help='native runner: print the fdlp_job_stats of the JOB (timings of its phases) to stdout')
     parser.add_argument('--mapped_output', action='store_true',
                         help='native runner: the features go from the kernel straight into pinned host memory '
                              '(no D2H copy)')
@@ -316,6 +318,7 @@ def _run_native(args, cfg, device, noise, snr, diff):
     o.out_mapped = int(bool(getattr(args, 'mapped_output', False)))
     st = _lib.FdlpJobStatsC()
     sys.stdout.flush()
+    t_call = time.time()
     rc = _lib.lib.fdlp_job_run(ctypes.byref(c), int(device), args.scp.encode(), args.outfile.encode(),
                                ctypes.byref(o), ctypes.byref(st))
     if rc != _lib.FDLP_OK:
@@ -327,6 +330,10 @@ def _run_native(args, cfg, device, noise, snr, diff):
         _lib.check(rc)
     global LAST_JOB_STATS
     LAST_JOB_STATS = {k: getattr(st, k) for k, _ in st._fields_}
+    LAST_JOB_STATS["call_seconds"] = time.time() - t_call  # includes the HIP runtime start of a cold process
+    if getattr(args, 'job_stats', False):
+        import json
+        print('%s: job stats %s' % (sys.argv[0], json.dumps(LAST_JOB_STATS)))
     _report_skips(st.n_lines, st.n_skipped)
     return None
 
@@ -340,11 +347,31 @@ def native_eligible(args, return_feats=False):
     return args.host_runner == 'native' and args.add_reverb in (None, '', 'clean') and not return_feats
 
 
+def narrow_visible_devices(args, env=os.environ):
+    """Before the HIP runtime starts: make the JOB's one GPU the only visible one (HIP_VISIBLE_DEVICES) and
+    address it as device 0, so a cold JOB process on an 8-GPU node initialises one device instead of
+    eight.  HIP_VISIBLE_DEVICES, if set, lists the candidates (its entries are kept, one is chosen); it
+    indexes into ROCR_VISIBLE_DEVICES when that is set.  Returns the narrowed args (device = 0)."""
+    dev = resolve_device(args)
+    hip = env.get("HIP_VISIBLE_DEVICES")
+    if hip is not None:
+        ids = [x.strip() for x in hip.split(",") if x.strip()]
+        if dev >= len(ids):
+            return args  # out of range: let HIP report it
+        env["HIP_VISIBLE_DEVICES"] = ids[dev]
+    else:
+        env["HIP_VISIBLE_DEVICES"] = str(dev)
+    args.device, args.device_rr = 0, None
+    return args
+
+
 def main(argv=None):
     args = build_parser().parse_args(argv)
     if native_eligible(args) and "torch" not in sys.modules:
         from speech_recognition_tools_amd import _hip_runtime
         _hip_runtime.TORCH = False  # before anything loads libfdlp_hip.so: a cold JOB skips importing torch
+        if "CUDA_VISIBLE_DEVICES" not in os.environ:
+            args = narrow_visible_devices(args)
     start_time = time.time()
     print('%s: Extracting features....' % sys.argv[0])
     sys.stdout.flush()

@@ -97,3 +97,19 @@ def test_native_cli_process_never_imports_torch(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert "TORCH False" in r.stdout, r.stdout + r.stderr
     assert "RESULT" in r.stdout, r.stdout + r.stderr
+
+
+def test_native_jobs_open_only_their_gpu(monkeypatch):
+    """A cold native JOB narrows HIP_VISIBLE_DEVICES to its own GPU before the HIP runtime starts (one device
+    initialised instead of every GPU of the node) and addresses it as device 0."""
+    from speech_recognition_tools_amd.featgen.computeFDLPSpectrogram import build_parser, narrow_visible_devices
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "LOCAL_RANK"):
+        monkeypatch.delenv(v, raising=False)
+    env = {}
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
+    a = narrow_visible_devices(build_parser().parse_args(["a.scp", "o", "--device_rr=11,8"]), env)
+    assert env["HIP_VISIBLE_DEVICES"] == "2" and a.device == 0 and a.device_rr is None
+    env = {"HIP_VISIBLE_DEVICES": "4,5,6,7"}
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "4,5,6,7")
+    a = narrow_visible_devices(build_parser().parse_args(["a.scp", "o", "--device_rr=2,4"]), env)
+    assert env["HIP_VISIBLE_DEVICES"] == "5" and a.device == 0
