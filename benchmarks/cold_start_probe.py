@@ -40,11 +40,15 @@ def main():
     hip.hipDeviceSynchronize()
     t["device_open_s"] = time.perf_counter() - t1
     cfg = FeatureConfig.wsj()
-    t1 = time.perf_counter()
-    c, keep = cfg.to_c(2048)
-    h = ctypes.c_void_p()
-    _lib.check(_lib.lib.fdlp_plan_create(ctypes.byref(c), 0, ctypes.byref(h)))
-    t["plan_create_s"] = time.perf_counter() - t1
+    for key, mf, dev in (("plan_host_only_s", 2048, -1), ("plan_create_64_frames_s", 64, 0),
+                         ("plan_create_s", 2048, 0)):
+        t1 = time.perf_counter()
+        c, keep = cfg.to_c(mf)
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib.fdlp_plan_create(ctypes.byref(c), dev, ctypes.byref(h)))
+        t[key] = time.perf_counter() - t1
+        if key != "plan_create_s":
+            _lib.lib.fdlp_plan_destroy(h)
     # one batch of 64 x 4 s utterances, twice (the first one loads the kernels' code objects)
     from bench import utterance_pcm
     entries = [("u%d" % i, 64000, 10 + i) for i in range(64)]

@@ -741,10 +741,9 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   if (hipMalloc((void**)&p->ws.z, sizeof(double2) * F * p->nfft_c) != hipSuccess ||
       hipMalloc((void**)&p->ws.dct, sizeof(double) * F * N) != hipSuccess ||
       hipMalloc((void**)&p->ws.r, sizeof(double) * items * p->nlags * (p->cplx ? 2 : 1)) != hipSuccess ||
-      hipMalloc((void**)&p->ws.a, sizeof(double) * items * (p->p + 1)) != hipSuccess ||
       hipMalloc((void**)&p->ws.gg, sizeof(double) * items) != hipSuccess ||
       (d.lpc_split && hipMalloc((void**)&p->ws.a_pad, sizeof(double) * items * d.lpc_astride) != hipSuccess) ||
-      hipMalloc((void**)&p->ws.cep, sizeof(double) * items * M) != hipSuccess ||
+      (p->modspec && hipMalloc((void**)&p->ws.cep, sizeof(double) * items * M) != hipSuccess) ||
       hipMalloc((void**)&p->ws.env, sizeof(double) * items * p->kk) != hipSuccess ||
       (p->sk_avail && hipMalloc((void**)&p->r_up, sizeof(double) * items * p->nlags) != hipSuccess) ||
       (p->vs_avail && hipMalloc((void**)&p->r_flat, sizeof(double) * items * p->nlags) != hipSuccess) ||
@@ -1055,6 +1054,15 @@ int fdlp_autocorr_path(const fdlp_plan* p) {
 int fdlp_set_debug(fdlp_plan* p, int32_t keep_intermediates) {
   if (!p) return fail(FDLP_E_INVALID, "fdlp_set_debug: null plan");
   p->debug_intermediates = keep_intermediates != 0;
+  // a [items, p+1] and cep [items, M] exist only for debugging (and cep for the modspec output): allocated
+  // here, not at plan creation (for REVERB's M = 450 the two are ~0.8 GB at 2048 frames)
+  if (p->debug_intermediates && p->device >= 0) {
+    DeviceGuard dg(p->device);
+    HIP_TRY(dg.status());
+    const size_t items = (size_t)p->max_frames * p->B;
+    if (!p->ws.a) HIP_TRY(hipMalloc((void**)&p->ws.a, sizeof(double) * items * (p->p + 1)));
+    if (!p->ws.cep) HIP_TRY(hipMalloc((void**)&p->ws.cep, sizeof(double) * items * p->M));
+  }
   return FDLP_OK;
 }
 
@@ -1085,6 +1093,8 @@ int fdlp_debug_fetch_range(fdlp_plan* p, int32_t f0, int32_t n, double* dct, dou
   HIP_TRY(dg.status());
   HIP_TRY(hipDeviceSynchronize());
   const size_t items = (size_t)n * p->B, it0 = (size_t)f0 * p->B;
+  if ((a && !p->ws.a) || (cep && !p->ws.cep))
+    return fail(FDLP_E_INVALID, "fdlp_debug_fetch: a / cep are kept only after fdlp_set_debug(plan, 1)");
   if (dct) HIP_TRY(hipMemcpy(dct, p->ws.dct + (size_t)f0 * p->N, sizeof(double) * n * (size_t)p->N, hipMemcpyDeviceToHost));
   if (r) HIP_TRY(hipMemcpy(r, p->ws.r + it0 * p->nlags, sizeof(double) * items * p->nlags, hipMemcpyDeviceToHost));
   if (a) HIP_TRY(hipMemcpy(a, p->ws.a + it0 * (p->p + 1), sizeof(double) * items * (p->p + 1), hipMemcpyDeviceToHost));
