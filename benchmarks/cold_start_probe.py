@@ -47,6 +47,9 @@ def main():
         h = ctypes.c_void_p()
         _lib.check(_lib.lib.fdlp_plan_create(ctypes.byref(c), dev, ctypes.byref(h)))
         t[key] = time.perf_counter() - t1
+        ph = np.zeros(5)
+        _lib.check(_lib.lib.fdlp_plan_setup_times(h, _lib.ptr(ph, ctypes.c_double)))
+        t[key + "_phases(host,upload,lpc_setup,workspace,total)"] = [round(float(v), 4) for v in ph]
         if key != "plan_create_s":
             _lib.lib.fdlp_plan_destroy(h)
     # one batch of 64 x 4 s utterances, twice (the first one loads the kernels' code objects)
@@ -75,7 +78,7 @@ def main():
         t[key] = time.perf_counter() - t1
     _lib.lib.fdlp_plan_destroy(h)
     t["total_s"] = time.perf_counter() - T0
-    print(json.dumps({k: round(v, 4) for k, v in t.items()}))
+    print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in t.items()}))
 
 
 if __name__ == "__main__":

@@ -198,6 +198,10 @@ int fdlp_debug_fetch_range(fdlp_plan* plan, int32_t first_frame, int32_t n_frame
 #define FDLP_NUM_STAGES 5
 int fdlp_set_profiling(fdlp_plan* plan, int32_t enable);
 int fdlp_stage_times(fdlp_plan* plan, double* ms_sum /* [FDLP_NUM_STAGES] */, int32_t* n_calls);
+/* Seconds fdlp_plan_create spent in: [0] host tables (filterbank, structured-autocorrelation tables,
+ * weights), [1] device open + table uploads, [2] LPC kernel launch setup, [3] workspace allocation,
+ * [4] total (a cold JOB's fixed cost, benchmarks/cold_start_probe.py; ABI 4). */
+int fdlp_plan_setup_times(const fdlp_plan* plan, double* sec /* [5] */);
 
 /* ---- stage entry points (the features.py helpers, batched on the device) --------------- */
 /* scipy.fftpack.dct(x)/sqrt(2N) of n_rows windowed frames [n_rows, N] (computeFDLPSpectrogram

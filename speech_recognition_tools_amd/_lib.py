@@ -133,6 +133,7 @@ SIGNATURES = {
     "fdlp_set_lpc_path": (c_i32, [c_p, c_i32]),
     "fdlp_set_pipeline": (c_i32, [c_p, c_i32]),
     "fdlp_stage_times": (c_i32, [c_p, P_dbl, P_i32]),
+    "fdlp_plan_setup_times": (c_i32, [c_p, P_dbl]),
     "fdlp_dct_rows": (c_i32, [c_p, c_p, c_i32, c_p, c_p]),
     "fdlp_lpc_rows": (c_i32, [c_p, c_p, c_i32, c_p, c_p, c_p, c_p]),
     "fdlp_cepstrum_rows": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_i32, c_p, c_p]),

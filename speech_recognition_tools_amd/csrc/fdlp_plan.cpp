@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <new>
 #include <string>
@@ -331,6 +332,8 @@ struct StagingHost {
 struct fdlp_plan {
   fdlp_config cfg{};
   int device = 0;
+  double setup_s[5] = {0, 0, 0, 0, 0};  // creation phases: host tables, device open + uploads, LPC launch
+                                        // setup, workspace, total (fdlp_plan_setup_times)
   // geometry (computeFDLPSpectrogram.py / features.py float expressions)
   int N = 0, nfft = 0, hop = 0, sp_b = 0, sp_f = 0, ext = 0, env_nfft = 0, kk = 0, kkb2 = 0, ola_hop = 0;
   int B = 0, p = 0, M = 0, nlags = 0, Me = 0, ncol = 0;
@@ -502,6 +505,14 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   if (c.max_frames < 1) return fail(FDLP_E_INVALID, "max_frames must be >= 1");
   auto* p = new (std::nothrow) fdlp_plan;
   if (!p) return fail(FDLP_E_NOMEM, "out of memory");
+  const auto t_begin = std::chrono::steady_clock::now();
+  auto t_last = t_begin;
+  auto phase = [&](int k) {  // seconds since the previous phase boundary into setup_s[k]
+    const auto t = std::chrono::steady_clock::now();
+    p->setup_s[k] = std::chrono::duration<double>(t - t_last).count();
+    p->setup_s[4] = std::chrono::duration<double>(t - t_begin).count();
+    t_last = t;
+  };
   p->cfg = c;
   p->cfg.lifter = nullptr;
   p->device = device;
@@ -682,9 +693,11 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
 
   p->max_frames = c.max_frames;
   if (device < 0) {  // host-only plan: geometry, filterbank, weights and OLA tables, no compute
+    phase(0);
     *out = p;
     return FDLP_OK;
   }
+  phase(0);
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) PLAN_FAIL(FDLP_E_HIP, "no HIP device visible");
   if (device < 0 || device >= ndev) PLAN_FAIL(FDLP_E_INVALID, "device index out of range");
@@ -732,8 +745,10 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
     }
   }
 
+  phase(1);
   // launch geometry of the persistent LPC kernel for this device (occupancy, large-LDS attribute)
   if (fdlp::prepare_lpc_env(d) != hipSuccess) PLAN_FAIL(FDLP_E_HIP, "LPC kernel launch setup failed");
+  phase(2);
 
   // workspace
   const size_t F = (size_t)c.max_frames, items = F * p->B;
@@ -759,9 +774,16 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
       hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&p->aux_stream, hipStreamNonBlocking) != hipSuccess)
     PLAN_FAIL(FDLP_E_NOMEM, "workspace allocation failed (reduce max_frames)");
+  phase(3);
 #undef PLAN_FAIL
 #undef PLAN_TRY
   *out = p;
+  return FDLP_OK;
+}
+
+int fdlp_plan_setup_times(const fdlp_plan* p, double* sec) {
+  if (!p || !sec) return fail(FDLP_E_INVALID, "fdlp_plan_setup_times: bad args");
+  for (int k = 0; k < 5; ++k) sec[k] = p->setup_s[k];
   return FDLP_OK;
 }
 
