@@ -359,6 +359,9 @@ def parse_args(argv=None):
                     help="utterances per CPU-baseline process (default: about 10 s of oracle time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-transfers", action="store_true", help="skip the PCIe-inclusive timed pass")
+    ap.add_argument("--xfer-d2h-streams", type=int, default=1, help="PCIe pass: device-to-host copy streams")
+    ap.add_argument("--xfer-compute-streams", type=int, default=0,
+                    help="PCIe pass: compute streams for the batches in flight (0: one per batch)")
     ap.add_argument("--pipeline", type=int, default=None, help="sub-batches over two streams (plan default 1)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="device batches in flight per GPU: independent plans on their own HIP streams, each "
@@ -521,11 +524,15 @@ def main():
         pcm_d = [pcm, torch.empty_like(pcm)] if B == 1 else pcms
         out_d = [out, torch.empty_like(out)] if B == 1 else outs
         out_h = [torch.empty(out.shape, dtype=out.dtype).pin_memory() for _ in range(NB)]
-        # one D2H stream per buffer set: a device-to-host copy on one SDMA engine runs at ~13 GB/s (rocprofv3
-        # memory-copy trace, profiles/r03g_*), so the batches' copy-outs go to separate streams / engines
+        # streams: H2D, D2H (--xfer-d2h-streams, batch b on b mod that) and compute (--xfer-compute-streams,
+        # default one per batch in flight).  The process has GPU_MAX_HW_QUEUES (4) hardware queues: streams
+        # beyond that share queues, and a copy queued behind another stream's kernels waits for them
         s_in = torch.cuda.Stream(dev)
-        s_outs = [torch.cuda.Stream(dev) for _ in range(NB)]
-        comp = [torch.cuda.current_stream(dev)] * 2 if B == 1 else streams
+        nd = max(1, args.xfer_d2h_streams)
+        s_outs = [torch.cuda.Stream(dev) for _ in range(nd)]
+        s_outs = [s_outs[b % nd] for b in range(NB)]
+        nc = args.xfer_compute_streams or B
+        comp = [torch.cuda.current_stream(dev)] * 2 if B == 1 else [streams[b % nc] for b in range(B)]
         ev_in = [torch.cuda.Event() for _ in range(NB)]
         ev_done = [torch.cuda.Event() for _ in range(NB)]
         ev_out = [torch.cuda.Event() for _ in range(NB)]
@@ -574,7 +581,8 @@ def main():
                 "note": "every batch's PCM copied in from pinned host memory and its float32 features copied back "
                         "every step (%s); not the headline (inputs resident in HBM)" %
                         ("double-buffered on two copy streams" if B == 1 else
-                         "%d batches in flight, one H2D stream and one D2H stream per batch" % B)}
+                         "%d batches in flight on %d compute streams, one H2D stream, %d D2H stream(s)" %
+                         (B, nc, nd))}
 
     audio_h = world * args.steps * B * audio_s / 3600.0
     value = audio_h / elapsed

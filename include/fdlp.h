@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define FDLP_ABI_VERSION 4
+#define FDLP_ABI_VERSION 5
 
 enum {
   FDLP_OK = 0,
@@ -168,6 +168,15 @@ int fdlp_autocorr_path(const fdlp_plan* plan);
 #define FDLP_LPC_AUTO 0
 #define FDLP_LPC_LDS 1
 int fdlp_set_lpc_path(fdlp_plan* plan, int32_t path);
+/* DCT stage (ABI 5).  FDLP_DCT_AUTO (plan default): for the recipes' frame length N = 24000 one kernel per
+ * frame (dct_frame_kernel: the packed 12000-point FFT as three in-register passes with LDS exchanges,
+ * D written once); other N, and FDLP_DCT_FOUR_STEP, the two four-step kernels through the Z workspace
+ * (allocated when first needed).  fdlp_dct_path returns FDLP_DCT_FRAME or FDLP_DCT_FOUR_STEP. */
+#define FDLP_DCT_AUTO 0
+#define FDLP_DCT_FOUR_STEP 1
+#define FDLP_DCT_FRAME 2
+int fdlp_set_dct_path(fdlp_plan* plan, int32_t path);
+int fdlp_dct_path(const fdlp_plan* plan);
 /* Lower-skirt / flat-top / upper-skirt split of every band, [0,m1) [m1,m2) [m2,N), used by the
  * STRUCTURED path; FDLP_E_INVALID when the filterbank does not have it. */
 int fdlp_plan_regions(const fdlp_plan* plan, int32_t* m1, int32_t* m2);

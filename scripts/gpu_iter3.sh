@@ -2,14 +2,14 @@
 # One iteration on a GPU box: selected parity tests, bench lines of the given configs, and optionally a
 # kernel trace (+ PMC passes) of one config's bench command.  Big rocpd databases are deleted after their
 # summaries are written (gpurun copies back <= 64 MiB of gpurun_out/).
-#   PYTEST_SEL="tests/test_gpu_parity.py -k reverb" BENCH_CONFIGS="reverb wsj" TRACE=reverb PMC=1 TAG=r03c
+#   PYTEST_SEL="tests/test_gpu_parity.py" PYTEST_K="reverb or dct" BENCH_CONFIGS="reverb wsj" TRACE=reverb PMC=1 TAG=r03c
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${TAG:-r03x}
 O=gpurun_out/$TAG
 mkdir -p $O
 if [ -n "${PYTEST_SEL:-}" ]; then
-  timeout -k 10 900 python -u -m pytest $PYTEST_SEL -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest $PYTEST_SEL ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
   rc=$?
   echo "pytest rc=$rc"; grep -E "passed|failed|error" $O/pytest_gpu.log | tail -3; grep -E "FAILED|Error|assert" $O/pytest_gpu.log | head -20
   [ $rc -ge 1 ] && exit $rc

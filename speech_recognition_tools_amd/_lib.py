@@ -131,6 +131,8 @@ SIGNATURES = {
     "fdlp_plan_regions": (c_i32, [c_p, c_p, c_p]),
     "fdlp_plan_flat_events": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_i32]),
     "fdlp_set_lpc_path": (c_i32, [c_p, c_i32]),
+    "fdlp_set_dct_path": (c_i32, [c_p, c_i32]),
+    "fdlp_dct_path": (c_i32, [c_p]),
     "fdlp_set_pipeline": (c_i32, [c_p, c_i32]),
     "fdlp_stage_times": (c_i32, [c_p, P_dbl, P_i32]),
     "fdlp_plan_setup_times": (c_i32, [c_p, P_dbl]),
@@ -181,7 +183,7 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.fdlp_abi_version() != 4:
+    if lib.fdlp_abi_version() != 5:
         raise ImportError("libfdlp_hip.so ABI mismatch")
     return lib
 

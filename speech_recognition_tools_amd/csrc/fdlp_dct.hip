@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <vector>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -432,6 +433,325 @@ __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const doub
     dct[(int64_t)f * N + k] = (w1.x * V1.x - w1.y * V1.y) * scale2;
     dct[(int64_t)f * N + k + M] = (w2.x * V2.x - w2.y * V2.y) * scale2;
   }
+}
+
+// -----------------------------------------------------------------------------------------
+// 3. The recipes' DCT (N = 24000) in ONE kernel per frame: the packed length-M = 12000 complex FFT
+//    as three in-register passes M = A x B x C = 20 x 24 x 25, q = BC q1 + C q2 + q3,
+//    k = k1 + A k2a + AB k2b:
+//      pass 1, thread (q2, q3): DFT_A over q1 of the gathered samples, twiddle W_M^{k1 (C q2 + q3)}
+//      pass 2, thread (k1, q3): DFT_B over q2, twiddle W_BC^{k2a q3}
+//      pass 3, thread (k1, k2a): DFT_C over q3 -> X[k]; real-FFT unpack with X[M - k] and the
+//              Makhoul post-twiddle -> D[k], D[k + M]
+//    The 12000 values stay in registers (one task per thread and pass); between passes they move
+//    through a 12000-double LDS image, real parts first, then imaginary parts (96 KB instead of 192).
+//    Pass-3 tasks are laid out so the task holding X[M - k] sits in the adjacent lane (lane ^ 1): the
+//    unpack takes it by DPP quad_perm.  No Z intermediate in HBM: the frame is read once and D written
+//    once (the four-step pair above moves Z = 384 KB per frame through HBM).
+// -----------------------------------------------------------------------------------------
+namespace dct1 {
+constexpr int kA = 20, kB = 24, kC = 25, kM = kA * kB * kC, kBC = kB * kC, kAC = kA * kC, kAB = kA * kB;
+constexpr int kThreads = 640;  // >= max(BC, AC, AB) tasks
+static_assert(kM == 12000 && kBC <= kThreads && kAC <= kThreads && kAB <= kThreads, "task layout");
+// table offsets (double2) in c.dct1_tw / LDS: W_M^b (b < BC), W_A^a, W_BC^e, rtw[lo], rtw[AB h],
+// post[lo], post[AB h]  (lo < AB, h < C)
+constexpr int kTwM = 0, kTwA = kTwM + kBC, kTwBC = kTwA + kA, kRtLo = kTwBC + kBC, kRtHi = kRtLo + kAB,
+              kPwLo = kRtHi + kC, kPwHi = kPwLo + kAB, kTabs = kPwHi + kC;
+
+// cos / sin of 2 pi e / n, evaluated by the compiler (Taylor series on [0, pi/4] after an exact
+// integer quadrant / octant reduction); used for the in-register radix twiddles
+constexpr double kHalfPi = 1.57079632679489661923;
+constexpr double tcos(double x) {
+  double x2 = x * x, term = 1.0, s = 1.0;
+  for (int i = 1; i < 16; ++i) { term *= -x2 / ((2.0 * i - 1.0) * (2.0 * i)); s += term; }
+  return s;
+}
+constexpr double tsin(double x) {
+  double x2 = x * x, term = x, s = x;
+  for (int i = 1; i < 16; ++i) { term *= -x2 / ((2.0 * i) * (2.0 * i + 1.0)); s += term; }
+  return s;
+}
+constexpr double qcos(long r, long n) {  // cos(pi/2 * r / n), 0 <= r <= n
+  return 2 * r <= n ? tcos(kHalfPi * ((double)r / (double)n)) : tsin(kHalfPi * ((double)(n - r) / (double)n));
+}
+constexpr double root_re(long e, long n) {  // cos(2 pi e / n)
+  e = ((e % n) + n) % n;
+  const long q = (4 * e) / n, r = 4 * e - q * n;
+  const double cr = qcos(r, n), sr = qcos(n - r, n);
+  return q == 0 ? cr : q == 1 ? -sr : q == 2 ? -cr : sr;
+}
+constexpr double root_im(long e, long n) {  // -sin(2 pi e / n): forward-DFT root W_n^e
+  e = ((e % n) + n) % n;
+  const long q = (4 * e) / n, r = 4 * e - q * n;
+  const double cr = qcos(r, n), sr = qcos(n - r, n);
+  return -(q == 0 ? sr : q == 1 ? cr : q == 2 ? -sr : -cr);
+}
+template <int N>
+struct Roots {
+  double re[N], im[N];
+  constexpr Roots() : re(), im() {
+    for (int e = 0; e < N; ++e) { re[e] = root_re(e, N); im[e] = root_im(e, N); }
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void rdft(double2 (&v)[N]);
+
+// N = P Q: n = Q p + q, k = kp + P kq; P-point DFTs over p, twiddle W_N^{q kp}, Q-point DFTs over q
+template <int P, int Q>
+__device__ __forceinline__ void rdft_pq(double2 (&v)[P * Q]) {
+  constexpr int N = P * Q;
+  constexpr Roots<N> W{};
+  double2 t[N];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    double2 w[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) w[p] = v[Q * p + q];
+    rdft<P>(w);
+#pragma unroll
+    for (int kp = 0; kp < P; ++kp) {
+      const int e = (q * kp) % N;
+      t[q * P + kp] = e == 0 ? w[kp] : cmul(w[kp], make_double2(W.re[e], W.im[e]));
+    }
+  }
+#pragma unroll
+  for (int kp = 0; kp < P; ++kp) {
+    double2 w[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) w[q] = t[q * P + kp];
+    rdft<Q>(w);
+#pragma unroll
+    for (int kq = 0; kq < Q; ++kq) v[kp + P * kq] = w[kq];
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void rdft(double2 (&v)[N]) {
+  if constexpr (N == 2 || N == 3 || N == 4 || N == 5) bfly_c<N>(v);
+  else if constexpr (N == 6) rdft_pq<2, 3>(v);
+  else if constexpr (N == 20) rdft_pq<4, 5>(v);
+  else if constexpr (N == 24) rdft_pq<4, 6>(v);
+  else if constexpr (N == 25) rdft_pq<5, 5>(v);
+  else static_assert(N == 2, "radix not instantiated");
+}
+
+__device__ __forceinline__ double2 swap_pair(double2 v) {  // value of lane ^ 1 (DPP quad_perm [1,0,3,2])
+  return make_double2(dpp_f64<0xB1>(v.x), dpp_f64<0xB1>(v.y));
+}
+
+// pass-3 task of lane t (< AB): (k1, k2a) and its pairing mode (0: partner in lane ^ 1,
+// 1: X[M - k] is its own register (C - k2b) mod C, 2: its own register C - 1 - k2b)
+__device__ __forceinline__ void pass3_task(int t, int& k1, int& k2a, int& mode) {
+  const int p = t >> 1, s = t & 1;
+  mode = 0;
+  if (p < 9 * kB) {                 // k1 in [1, 10) with (20 - k1, 23 - k2a)
+    const int a = 1 + p % 9, b = p / 9;
+    k1 = s ? kA - a : a;
+    k2a = s ? kB - 1 - b : b;
+  } else if (p < 9 * kB + kB / 2) {  // k1 = 10 with (10, 23 - k2a)
+    const int b = p - 9 * kB;
+    k1 = kA / 2;
+    k2a = s ? kB - 1 - b : b;
+  } else if (p < 9 * kB + kB - 1) {  // k1 = 0: (0, k2a) with (0, 24 - k2a), k2a in [1, 12)
+    const int b = p - (9 * kB + kB / 2) + 1;
+    k1 = 0;
+    k2a = s ? kB - b : b;
+  } else {                           // (0, 0) and (0, 12): their own partners
+    k1 = 0;
+    k2a = s ? kB / 2 : 0;
+    mode = s ? 2 : 1;
+  }
+}
+}  // namespace dct1
+
+__global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, const void* __restrict__ pcm,
+                                                                   int pcm_kind, const int16_t* __restrict__ noise,
+                                                                   const FrameDesc* __restrict__ frames,
+                                                                   const double* __restrict__ dense_rows,
+                                                                   double scale2, double* __restrict__ dct) {
+  using namespace dct1;
+  __shared__ double xch[kM];
+  __shared__ double2 tab[kTabs + kC];  // tables + the (0, 0) task's X (pass 3)
+  const int t = threadIdx.x;
+  const int f = blockIdx.x;
+  constexpr int N = 2 * kM;
+  for (int q = t; q < kTabs; q += kThreads) tab[q] = c.dct1_tw[q];
+
+  // ---- pass 1: thread n2 = C q2 + q3 gathers z[BC q1 + n2] = v[2q] + i v[2q+1] (Makhoul order) ----
+  double2 y1[kA];
+  if (t < kBC && !dense_rows) {
+    const FrameDesc fd = frames[f];
+    const int64_t t0 = (int64_t)fd.k * c.hop - c.ext;
+    const bool fast = pcm_kind == 0 && fd.noise_off < 0 && t0 >= 0 && t0 + N <= fd.T;
+    if (fast) {
+      const int16_t* xs = (const int16_t*)pcm + fd.pcm_off + t0;
+#pragma unroll
+      for (int q1 = 0; q1 < kA; ++q1) {
+        const int q = kBC * q1 + t;
+        // v[2q] = x[4q], v[2q+1] = x[4q+2] in the first half, mirrored (x[2N-1-4q], x[2N-3-4q]) after
+        const int m0 = 4 * q1 < kA * 2 ? 4 * q : 2 * N - 1 - 4 * q;
+        const int m1 = 4 * q1 < kA * 2 ? 4 * q + 2 : 2 * N - 3 - 4 * q;
+        y1[q1].x = __dmul_rn((double)xs[m0], c.hamming[m0]);
+        y1[q1].y = __dmul_rn((double)xs[m1], c.hamming[m1]);
+      }
+    }
+  }
+  // general frames (reflect padding, noise mixing, the diff filter, fp64 input, dense rows): the
+  // samples are staged through xch by a rolled loop (the general gather is too large to unroll 40x),
+  // real parts then imaginary parts; the branch is uniform over the workgroup
+  const bool fast_wg = !dense_rows && pcm_kind == 0 && [&] {
+    const FrameDesc fd0 = frames[f];
+    const int64_t s0 = (int64_t)fd0.k * c.hop - c.ext;
+    return fd0.noise_off < 0 && s0 >= 0 && s0 + N <= fd0.T;
+  }();
+  if (!fast_wg) {
+    FrameDesc fd;
+    if (!dense_rows) fd = frames[f];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      for (int q = t; q < kM; q += kThreads) xch[q] = makhoul_sample(c, fd, 2 * q + h, f, pcm, pcm_kind, noise, dense_rows);
+      __syncthreads();
+      if (t < kBC) {
+#pragma unroll
+        for (int q1 = 0; q1 < kA; ++q1) {
+          const double v = xch[kBC * q1 + t];
+          if (h) y1[q1].y = v; else y1[q1].x = v;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (t < kBC) rdft<kA>(y1);
+  __syncthreads();  // tables
+  if (t < kBC) {
+#pragma unroll
+    for (int k1 = 1; k1 < kA; ++k1) {  // W_M^{k1 n2}, k1 n2 = BC a + b: W_A^a W_M^b
+      const int e = k1 * t, a = e / kBC, b = e - kBC * a;
+      y1[k1] = cmul(y1[k1], cmul(tab[kTwA + a], tab[kTwM + b]));
+    }
+  }
+  // ---- exchange 1: [k1][n2] -> thread (k1, q3) reads q2 ----
+  const int k1b = t / kC, q3 = t - kC * (t / kC);
+  double2 y2[kB];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (t < kBC) {
+#pragma unroll
+      for (int k1 = 0; k1 < kA; ++k1) xch[k1 * kBC + t] = h ? y1[k1].y : y1[k1].x;
+    }
+    __syncthreads();
+    if (t < kAC) {
+#pragma unroll
+      for (int q2 = 0; q2 < kB; ++q2) {
+        const double v = xch[k1b * kBC + kC * q2 + q3];
+        if (h) y2[q2].y = v; else y2[q2].x = v;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- pass 2: DFT_B over q2, twiddle W_BC^{k2a q3}; exchange 2: [k2a][k1][q3] ----
+  if (t < kAC) {
+    rdft<kB>(y2);
+#pragma unroll
+    for (int k2a = 1; k2a < kB; ++k2a) y2[k2a] = cmul(y2[k2a], tab[kTwBC + k2a * q3]);
+  }
+  int k1, k2a, mode;
+  dct1::pass3_task(t < kAB ? t : 0, k1, k2a, mode);
+  double2 y3[kC];
+  const int a3 = k2a * kAC + k1 * kC;
+  if (t < kAC) {
+#pragma unroll
+    for (int j = 0; j < kB; ++j) xch[j * kAC + t] = y2[j].x;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kC; ++j) y3[j].x = xch[a3 + j];
+  __syncthreads();
+  if (t < kAC) {
+#pragma unroll
+    for (int j = 0; j < kB; ++j) xch[j * kAC + t] = y2[j].y;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kC; ++j) y3[j].y = xch[a3 + j];
+  // ---- pass 3: DFT_C over q3 -> X[k1 + A k2a + AB k2b]; unpack with X[M - k] ----
+  if (t >= 64 * ((kAB + 63) / 64)) return;  // whole waves without pass-3 tasks
+  rdft<kC>(y3);
+  const int lo = k1 + kA * k2a;
+  const double2 rl = tab[kRtLo + lo], pl = tab[kPwLo + lo];
+  double* drow = dct + (int64_t)f * N;
+  // D[k], D[k + M] from V = X_k and W = X_{M-k} (E / O split of the packed FFT, Makhoul post-twiddle)
+  auto emit = [&](int j, double2 V, double2 W) {
+    const double2 E = make_double2(0.5 * (V.x + W.x), 0.5 * (V.y - W.y));
+    const double2 O = make_double2(0.5 * (V.y + W.y), -0.5 * (V.x - W.x));
+    const double2 rt = cmul(rl, tab[kRtHi + j]);
+    const double2 w1 = cmul(pl, tab[kPwHi + j]);
+    constexpr double hr = 0.70710678118654752440;  // post[k + M] = post[k] e^{-i pi / 4}
+    const double2 w2 = make_double2(hr * (w1.x + w1.y), hr * (w1.y - w1.x));
+    const double2 tt = cmul(rt, O);
+    const double2 V1 = make_double2(E.x + tt.x, E.y + tt.y);
+    const double2 V2 = make_double2(E.x - tt.x, E.y - tt.y);
+    const int k = lo + kAB * j;
+    drow[k] = (w1.x * V1.x - w1.y * V1.y) * scale2;
+    drow[k + kM] = (w2.x * V2.x - w2.y * V2.y) * scale2;
+  };
+  // pairs in lanes (2i, 2i+1) and the self-paired (0, 12) (mode 2): X_{M-k} is register C-1-j of the
+  // partner lane, or of the lane itself
+  const bool act = t < kAB && mode != 1;
+  if (mode == 1) {  // the one lane of task (0, 0) parks its X in LDS (read back by the same lane below)
+#pragma unroll
+    for (int j = 0; j < kC; ++j) tab[kTabs + j] = y3[j];
+  }
+  // j and C-1-j together, so both registers are dead after the pair (C odd: the middle one alone)
+#pragma unroll
+  for (int j = 0; j < (kC + 1) / 2; ++j) {
+    const int jm = kC - 1 - j;
+    const double2 a = y3[j], b = y3[jm];
+    const double2 sa = swap_pair(a), sb = swap_pair(b);  // every lane of the wave takes part in the DPP
+    if (act) {
+      emit(j, a, mode == 2 ? b : sb);
+      if (jm != j) emit(jm, b, mode == 2 ? a : sa);
+    }
+  }
+  if (mode == 1) {  // (0, 0): X_{M-k} = its own value (C - j) mod C, parked in LDS above
+#pragma unroll
+    for (int j = 0; j < kC; ++j) emit(j, tab[kTabs + j], tab[kTabs + (kC - j) % kC]);
+  }
+}
+
+// host tables of dct_frame_kernel (double2 [dct1::kTabs]); empty unless N = 24000 with the real FFT
+std::vector<double2> dct_frame_tables(int N) {
+  using namespace dct1;
+  std::vector<double2> tab;
+  if (N != 2 * kM) return tab;
+  tab.resize(kTabs);
+  const long double PI = 3.141592653589793238462643383279502884L;
+  auto root = [&](long long e, long long n) {  // W_n^e = exp(-2 pi i e / n)
+    const long double ang = -2.0L * PI * (long double)(e % n) / (long double)n;
+    return make_double2((double)cosl(ang), (double)sinl(ang));
+  };
+  auto post = [&](long long k) {  // exp(-i pi k / (2N))
+    const long double ang = -PI * (long double)k / (2.0L * (long double)N);
+    return make_double2((double)cosl(ang), (double)sinl(ang));
+  };
+  for (int b = 0; b < kBC; ++b) tab[kTwM + b] = root(b, kM);
+  for (int a = 0; a < kA; ++a) tab[kTwA + a] = root(a, kA);
+  for (int e = 0; e < kBC; ++e) tab[kTwBC + e] = root(e, kBC);
+  for (int lo = 0; lo < kAB; ++lo) { tab[kRtLo + lo] = root(lo, N); tab[kPwLo + lo] = post(lo); }
+  for (int h = 0; h < kC; ++h) { tab[kRtHi + h] = root((long long)kAB * h, N); tab[kPwHi + h] = post((long long)kAB * h); }
+  return tab;
+}
+
+hipError_t launch_dct_frame(const DevConsts& c, const void* pcm, int pcm_kind, const int16_t* noise,
+                            const FrameDesc* frames, const double* dense_rows, int nframes, double* dct,
+                            hipStream_t s) {
+  if (nframes <= 0) return hipSuccess;
+  if (!c.dct1_tw || c.N != 2 * dct1::kM || !c.real_fft || c.natural) return hipErrorInvalidValue;
+  const double sc2 = 2.0 / sqrt((double)(2 * c.N));
+  hipLaunchKernelGGL(dct_frame_kernel, dim3(nframes), dim3(dct1::kThreads), 0, s, c, pcm, pcm_kind, noise, frames,
+                     dense_rows, sc2, dct);
+  return hipGetLastError();
 }
 
 // -----------------------------------------------------------------------------------------

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace fdlp {
 
 constexpr int kMaxRadices = 16;
@@ -91,6 +93,7 @@ struct DevConsts {
                            // (scipy.fftpack.ifft of the real frame), bins [0, N/2), as double2 rows of N doubles
   int lpc_astride = 0;     // split Durbin: row stride of a_pad (the cepstrum kernel's a-area length,
                            // zero past p), so a row is one contiguous LDS-DMA copy
+  const double2* dct1_tw = nullptr;  // dct_frame_kernel tables (N = 24000 only; see dct_frame_tables)
 };
 
 }  // namespace fdlp
@@ -114,6 +117,11 @@ hipError_t launch_frames_dft1(const DevConsts& c, const DftPlan& d1, int N2, con
                               const double2* om1, hipStream_t s);
 hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const double2* z,
                            int nframes, double* dct, const double2* om2, hipStream_t s);
+// the recipes' DCT (N = 24000, real FFT) as one kernel per frame; hipErrorInvalidValue otherwise
+hipError_t launch_dct_frame(const DevConsts& c, const void* pcm, int pcm_kind, const int16_t* noise,
+                            const FrameDesc* frames, const double* dense_rows, int nframes, double* dct,
+                            hipStream_t s);
+std::vector<double2> dct_frame_tables(int N);
 hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* dense_rows,
                            int nframes_or_items, double* r, hipStream_t s);
 hipError_t launch_autocorr_structured(const DevConsts& c, const double* dct, int nframes, double* r,

@@ -348,6 +348,8 @@ struct fdlp_plan {
   double *d_fbank = nullptr, *d_hamming = nullptr, *d_weights = nullptr, *d_env_cos = nullptr,
          *d_env_win = nullptr, *d_tw1 = nullptr, *d_post = nullptr, *d_rtw = nullptr;
   double2 *d_om1 = nullptr, *d_om2 = nullptr;
+  double2* d_dct1 = nullptr;         // dct_frame_kernel tables (N = 24000)
+  int dct_path = FDLP_DCT_AUTO;      // fdlp_set_dct_path
   int *d_lo = nullptr, *d_hi = nullptr;
   // workspace
   int max_frames = 0;
@@ -385,6 +387,10 @@ struct fdlp_plan {
   int prof_calls = 0;
 };
 
+// the recipes' DCT as one kernel per frame (dct_frame_kernel) unless fdlp_set_dct_path chose the
+// two four-step kernels
+static bool dct_fused(const fdlp_plan* p) { return p->dc.dct1_tw && p->dct_path == FDLP_DCT_AUTO; }
+
 namespace {
 
 int drain_profile(fdlp_plan* p) {
@@ -413,7 +419,7 @@ int free_plan(fdlp_plan* p) {
   for (auto& ev : p->prof_pending)
     for (auto e : ev) (void)hipEventDestroy(e);
   void* devs[] = {p->d_fbank, p->d_hamming, p->d_weights, p->d_env_cos, p->d_env_win, p->d_tw1, p->d_post, p->d_rtw,
-                  p->d_om1, p->d_om2, p->d_lo, p->d_hi, p->ws.z, p->ws.dct, p->ws.r, p->ws.a, p->ws.gg,
+                  p->d_om1, p->d_om2, p->d_dct1, p->d_lo, p->d_hi, p->ws.z, p->ws.dct, p->ws.r, p->ws.a, p->ws.gg,
                   p->ws.cep, p->ws.env, p->ws.a_pad, p->d_frames, p->d_utts, p->d_sk_e, p->r_up, p->d_sk_snap,
                   p->d_sk_reg, p->d_faxis, p->r_flat, p->d_fl_ev, p->r_flat_part, p->d_fl_band};
   for (void* d : devs)
@@ -721,6 +727,10 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   PLAN_TRY(upload(&p->d_rtw, rtw.data(), rtw.size()));
   PLAN_TRY(upload(&p->d_om1, om1.data(), om1.size()));
   PLAN_TRY(upload(&p->d_om2, om2.data(), om2.size()));
+  if (p->real_fft && !p->cplx) {  // the recipes' N = 24000: one DCT kernel per frame
+    const std::vector<double2> dct1 = fdlp::dct_frame_tables(N);
+    if (!dct1.empty()) PLAN_TRY(upload(&p->d_dct1, dct1.data(), dct1.size()));
+  }
 
   fdlp::DevConsts& d = p->dc;
   d.B = p->B; d.N = N; d.hop = p->hop; d.ext = p->ext; d.p = p->p; d.nlags = p->nlags; d.M = M; d.Me = p->Me;
@@ -728,6 +738,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   d.fbank = p->d_fbank; d.lo = p->d_lo; d.hi = p->d_hi; d.hamming = p->d_hamming; d.weights = p->d_weights;
   d.env_cos = p->d_env_cos; d.env_win = p->d_env_win; d.tw1 = p->d_tw1; d.post = p->d_post;
   d.rtw = p->d_rtw; d.real_fft = p->real_fft ? 1 : 0; d.natural = p->cplx ? 1 : 0;
+  d.dct1_tw = p->d_dct1;
   if (p->sk_avail) {
     PLAN_TRY(upload(&p->d_sk_e, p->sk.e.data(), p->sk.e.size()));
     PLAN_TRY(upload(&p->d_sk_snap, p->sk.snap.data(), p->sk.snap.size()));
@@ -753,7 +764,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   // workspace
   const size_t F = (size_t)c.max_frames, items = F * p->B;
   p->max_frames = c.max_frames;
-  if (hipMalloc((void**)&p->ws.z, sizeof(double2) * F * p->nfft_c) != hipSuccess ||
+  if ((!dct_fused(p) && hipMalloc((void**)&p->ws.z, sizeof(double2) * F * p->nfft_c) != hipSuccess) ||
       hipMalloc((void**)&p->ws.dct, sizeof(double) * F * N) != hipSuccess ||
       hipMalloc((void**)&p->ws.r, sizeof(double) * items * p->nlags * (p->cplx ? 2 : 1)) != hipSuccess ||
       hipMalloc((void**)&p->ws.gg, sizeof(double) * items) != hipSuccess ||
@@ -942,11 +953,17 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     double* gg_dbg = p->debug_intermediates ? p->ws.gg + it0 : nullptr;
     double* cep_dbg = (p->debug_intermediates || p->modspec) ? p->ws.cep + it0 * p->M : nullptr;
     HIP_TRY(mark(0));
-    HIP_TRY(fdlp::launch_frames_dft1(p->dc, p->d1, p->d2.n, b->pcm_dev,
-                                     b->preprocess == FDLP_PRE_DIFF ? 2 : b->pcm_kind, b->noise_dev, p->d_frames + f0,
-                                     nullptr, n, p->ws.z + f0 * p->nfft_c, p->d_om1, st));
-    HIP_TRY(mark(1));
-    HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z + f0 * p->nfft_c, n, p->ws.dct + f0 * N, p->d_om2, st));
+    const int pcm_kind = b->preprocess == FDLP_PRE_DIFF ? 2 : b->pcm_kind;
+    if (dct_fused(p)) {  // one kernel per frame; the second DCT stage mark follows it directly
+      HIP_TRY(fdlp::launch_dct_frame(p->dc, b->pcm_dev, pcm_kind, b->noise_dev, p->d_frames + f0, nullptr, n,
+                                     p->ws.dct + f0 * N, st));
+      HIP_TRY(mark(1));
+    } else {
+      HIP_TRY(fdlp::launch_frames_dft1(p->dc, p->d1, p->d2.n, b->pcm_dev, pcm_kind, b->noise_dev, p->d_frames + f0,
+                                       nullptr, n, p->ws.z + f0 * p->nfft_c, p->d_om1, st));
+      HIP_TRY(mark(1));
+      HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z + f0 * p->nfft_c, n, p->ws.dct + f0 * N, p->d_om2, st));
+    }
     HIP_TRY(mark(2));
     if (p->cplx) {  // complex modulation: autocorrelation, LPC, cepstrum and the output columns
       const fdlp_config& c = p->cfg;
@@ -1062,6 +1079,24 @@ int fdlp_set_lpc_path(fdlp_plan* p, int32_t path) {
   return FDLP_OK;
 }
 
+int fdlp_set_dct_path(fdlp_plan* p, int32_t path) {
+  if (!p || (path != FDLP_DCT_AUTO && path != FDLP_DCT_FOUR_STEP))
+    return fail(FDLP_E_INVALID, "fdlp_set_dct_path: need a plan and FDLP_DCT_AUTO or FDLP_DCT_FOUR_STEP");
+  if (p->device < 0) return fail(FDLP_E_INVALID, "fdlp_set_dct_path: host-only plan");
+  DeviceGuard dg(p->device);
+  if (dg.status() != hipSuccess) return fail(FDLP_E_HIP, "hipSetDevice failed");
+  p->dct_path = path;
+  if (!dct_fused(p) && !p->ws.z &&
+      hipMalloc((void**)&p->ws.z, sizeof(double2) * (size_t)p->max_frames * p->nfft_c) != hipSuccess)
+    return fail(FDLP_E_NOMEM, "device workspace allocation failed");
+  return FDLP_OK;
+}
+
+int fdlp_dct_path(const fdlp_plan* p) {
+  if (!p) return fail(FDLP_E_INVALID, "fdlp_dct_path: null plan");
+  return dct_fused(p) ? FDLP_DCT_FRAME : FDLP_DCT_FOUR_STEP;
+}
+
 int fdlp_set_pipeline(fdlp_plan* p, int32_t n_sub) {
   if (!p || n_sub < 1) return fail(FDLP_E_INVALID, "fdlp_set_pipeline: need a plan and n_sub >= 1");
   p->pipeline = n_sub;
@@ -1135,6 +1170,10 @@ int fdlp_dct_rows(fdlp_plan* p, const double* x, int32_t n, double* y, void* str
   if (!p || !x || !y || n < 0 || p->device < 0) return fail(FDLP_E_INVALID, "fdlp_dct_rows: bad args or host-only plan");
   if (n > p->max_frames) return fail(FDLP_E_CAPACITY, "fdlp_dct_rows: more rows than max_frames");
   hipStream_t s = (hipStream_t)stream;
+  if (dct_fused(p)) {
+    HIP_TRY(fdlp::launch_dct_frame(p->dc, nullptr, 0, nullptr, nullptr, x, n, y, s));
+    return FDLP_OK;
+  }
   HIP_TRY(fdlp::launch_frames_dft1(p->dc, p->d1, p->d2.n, nullptr, 0, nullptr, nullptr, x, n, p->ws.z, p->d_om1, s));
   HIP_TRY(fdlp::launch_dft2_dct(p->dc, p->d2, p->d1.n, p->ws.z, n, y, p->d_om2, s));
   return FDLP_OK;

@@ -175,6 +175,20 @@ class FdlpPlan:
         Durbin kernel (the large-p fallback, an independent cross-check)."""
         check(lib.fdlp_set_lpc_path(self._h, self.LPC_PATHS[path]))
 
+    DCT_PATHS = {"auto": 0, "four_step": 1}
+
+    def set_dct_path(self, path: str = "auto"):
+        """'auto': the recipes' N = 24000 DCT as one kernel per frame (dct_frame_kernel), other N the
+        four-step pair; 'four_step': the two four-step kernels through the Z workspace."""
+        check(lib.fdlp_set_dct_path(self._h, self.DCT_PATHS[path]))
+
+    @property
+    def dct_path(self) -> str:
+        v = lib.fdlp_dct_path(self._h)
+        if v < 0:
+            check(v)
+        return {1: "four_step", 2: "frame"}[v]
+
     def regions(self):
         """(m1, m2) int32 arrays: band j's lower skirt [0,m1), flat top [m1,m2), upper skirt [m2,N)."""
         m1 = np.empty(self.B, dtype=np.int32)

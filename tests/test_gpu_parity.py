@@ -43,12 +43,13 @@ def _batch_inputs(meta, sig, z):
     return pcm, kw
 
 
-def run_gpu(meta, sig, z, support_eps=None, max_frames=256, debug=False, path="auto", lpc="auto"):
+def run_gpu(meta, sig, z, support_eps=None, max_frames=256, debug=False, path="auto", lpc="auto", dct="auto"):
     from speech_recognition_tools_amd import FdlpPlan, PyRandom
     cfg = feature_cfg(meta, support_eps)
     plan = FdlpPlan(cfg, device=0, max_frames=max_frames)
     plan.set_autocorr_path(path)
     plan.set_lpc_path(lpc)
+    plan.set_dct_path(dct)
     if debug:
         plan.set_debug(True)
     utts = meta["utts"]
@@ -228,6 +229,26 @@ def test_dct_rows_even_and_odd_lengths(fduration):
     y = plan.dct_rows(torch.from_numpy(x).cuda()).cpu().numpy()
     ref = scipy.fft.dct(x, type=2, axis=-1) / np.sqrt(2 * N)
     assert np.abs(y - ref).max() <= 1e-12 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("name", ["wsj", "wsj_diff", "chime4_noise", "reverb_rir_noise"])
+def test_dct_frame_kernel_matches_four_step(name):
+    """The single-kernel DCT (dct_frame_kernel, default at N = 24000) against the four-step kernel pair
+    on every frame of a golden set: plain int16 frames (the direct gather), reflect-padded edges, the
+    diff filter, noise mixing and fp64 (reverberated) input (the staged gather); then the features."""
+    meta, sig, ref, z = load_golden(name)
+    plan_f, res_f = run_gpu(meta, sig, z, debug=True)
+    assert plan_f.dct_path == "frame"
+    plan_4, res_4 = run_gpu(meta, sig, z, debug=True, dct="four_step")
+    assert plan_4.dct_path == "four_step"
+    # frames of the batch (a reverberated utterance may come out one sample shorter: a lower bound)
+    nf = sum(plan_f.geometry(sig[u].size - 1)[0] for u in meta["utts"])
+    d_f = plan_f.debug_fetch(nf, keys=("dct",))["dct"]
+    d_4 = plan_4.debug_fetch(nf, keys=("dct",))["dct"]
+    scale = np.abs(d_4).max(axis=-1, keepdims=True)
+    assert (np.abs(d_f - d_4) / scale).max() <= 1e-13
+    for u in meta["utts"]:
+        np.testing.assert_allclose(res_f[u][0], res_4[u][0], rtol=0, atol=TOL_UTT.get(u, 1e-8))
 
 
 @pytest.mark.parametrize("name", ["wsj", "reverb", "cli_default_mel"])
