@@ -216,7 +216,7 @@ def _latest_pmc(config="wsj"):
 
 PMC_FILE = _latest_pmc()
 # kernels of each timed stage (fdlp_stage_times), as rocprofv3 names them
-STAGE_KERNELS = {"dct": ("fdlp::frames_dft1", "fdlp::dft2_dct"),
+STAGE_KERNELS = {"dct": ("fdlp::dct_frame", "fdlp::frames_dft1", "fdlp::dft2_dct"),
                  "autocorr": {"structured": ("fdlp::ac_vsweep_kernel", "fdlp::ac_band_kernel"),
                               "structured_mfma": ("fdlp::ac_sweep_kernel", "fdlp::ac_band_kernel"),
                               "direct": ("fdlp::autocorr_kernel",)},

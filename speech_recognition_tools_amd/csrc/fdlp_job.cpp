@@ -778,7 +778,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
       copies.wait(slot_i);  // the pending copies target the old buffer
       std::vector<uint8_t> keep((size_t)pend.samples * elem);
       if (pend.samples) memcpy(keep.data(), sl.h_pcm, keep.size());
-      JOB_TRY(grow_pinned(&sl.h_pcm, &sl.pcm_cap, std::max(need, (size_t)c.max_frames * 18000 * elem)));
+      JOB_TRY(grow_pinned(&sl.h_pcm, &sl.pcm_cap, std::max(need, pin_smp * elem)));  // hop-based estimate; grow_pinned grows 3/2
       if (!keep.empty()) memcpy(sl.h_pcm, keep.data(), keep.size());
     }
     if (kind == FDLP_PCM_I16)
