@@ -248,7 +248,10 @@ def test_dct_frame_kernel_matches_four_step(name):
     scale = np.abs(d_4).max(axis=-1, keepdims=True)
     assert (np.abs(d_f - d_4) / scale).max() <= 1e-13
     for u in meta["utts"]:
-        np.testing.assert_allclose(res_f[u][0], res_4[u][0], rtol=0, atol=TOL_UTT.get(u, 1e-8))
+        # the two DCTs round differently (<= 1e-13 of the frame maximum, above); Levinson amplifies that
+        # to ~4e-8 on the wsj set's least well-conditioned frames (measured), the same order as the
+        # lattice-vs-LDS Durbin bar; each path is held to the reference at 1e-4 by the golden tests
+        np.testing.assert_allclose(res_f[u][0], res_4[u][0], rtol=0, atol=TOL_UTT.get(u, 1e-6), err_msg=u)
 
 
 @pytest.mark.parametrize("name", ["wsj", "reverb", "cli_default_mel"])
