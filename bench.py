@@ -512,62 +512,62 @@ def main():
     plan.set_profiling(False)
 
     # 3) PCIe-inclusive: PCM copied in from pinned host memory and float32 features back to pinned host
-    #    memory, every batch of every step.  B = 1: double buffered (copy-in / compute / copy-out of
-    #    consecutive steps on three streams); B > 1: each batch in flight has its own device buffers and
-    #    compute stream, the copies of one batch overlap the kernels of the others (one H2D and one D2H
-    #    stream).  `mapped` = the OLA kernel stores the features straight into the pinned host buffer
-    #    through its device mapping instead of a D2H copy (measured slower: reported, not used).
+    #    memory, every batch of every step.  Every batch in flight has two device buffer sets used on
+    #    alternate steps, so step s + 1's copy-in runs while step s computes and step s's copy-out while
+    #    step s + 1 computes (with one set per batch, every step's four copy-ins queued behind the previous
+    #    step's kernels on the one H2D stream: 31.9 ms per step against 23.4 computing, r03f).  One H2D
+    #    and one D2H stream (--xfer-d2h-streams); the compute of batch b stays on its own stream.
+    #    `mapped` = the OLA kernel stores the features straight into the pinned host buffer through its
+    #    device mapping instead of a D2H copy (measured slower: reported, not used).
     xfer = None
     if not args.no_transfers:
         pin_in = torch.from_numpy(pcm_host).pin_memory()
-        NB = 2 if B == 1 else B                          # device buffer sets
-        pcm_d = [pcm, torch.empty_like(pcm)] if B == 1 else pcms
-        out_d = [out, torch.empty_like(out)] if B == 1 else outs
+        NB = 2 * B                                       # device buffer sets: (batch, step parity)
+        pcm_d = [pcms[i // 2] if i % 2 == 0 else torch.empty_like(pcm) for i in range(NB)]
+        out_d = [outs[i // 2] if i % 2 == 0 else torch.empty_like(out) for i in range(NB)]
         out_h = [torch.empty(out.shape, dtype=out.dtype).pin_memory() for _ in range(NB)]
         # streams: H2D, D2H (--xfer-d2h-streams, batch b on b mod that) and compute (--xfer-compute-streams,
-        # default one per batch in flight).  The process has GPU_MAX_HW_QUEUES (4) hardware queues: streams
-        # beyond that share queues, and a copy queued behind another stream's kernels waits for them
+        # default one per batch in flight)
         s_in = torch.cuda.Stream(dev)
         nd = max(1, args.xfer_d2h_streams)
         s_outs = [torch.cuda.Stream(dev) for _ in range(nd)]
-        s_outs = [s_outs[b % nd] for b in range(NB)]
         nc = args.xfer_compute_streams or B
-        comp = [torch.cuda.current_stream(dev)] * 2 if B == 1 else [streams[b % nc] for b in range(B)]
+        comp = [torch.cuda.current_stream(dev)] if B == 1 else [streams[b % nc] for b in range(B)]
         ev_in = [torch.cuda.Event() for _ in range(NB)]
         ev_done = [torch.cuda.Event() for _ in range(NB)]
         ev_out = [torch.cuda.Event() for _ in range(NB)]
         for i in range(NB):
-            ev_done[i].record(comp[i])
-            ev_out[i].record(comp[i])
+            ev_done[i].record(comp[(i // 2) % len(comp)])
+            ev_out[i].record(comp[(i // 2) % len(comp)])
         it = [0]
         mapped = [False]
 
-        def xbatch(b):
-            s_in.wait_event(ev_done[b])                  # pcm_d[b] no longer read by its previous compute
+        def xbatch(b, i):
+            cs = comp[b % len(comp)]
+            s_in.wait_event(ev_done[i])                  # pcm_d[i] no longer read by its previous compute
             with torch.cuda.stream(s_in):
-                pcm_d[b].copy_(pin_in, non_blocking=True)
-                ev_in[b].record(s_in)
-            comp[b].wait_event(ev_in[b])
-            comp[b].wait_event(ev_out[b])                # out_d[b] copied out by its previous D2H
-            with torch.cuda.stream(comp[b]):
-                plans[b if B > 1 else 0].compute(pcm_d[b], lens, rng.randbits2(nj),
-                                                 out=out_h[b] if mapped[0] else out_d[b], **mix[b if B > 1 else 0])
-                ev_done[b].record(comp[b])
+                pcm_d[i].copy_(pin_in, non_blocking=True)
+                ev_in[i].record(s_in)
+            cs.wait_event(ev_in[i])
+            cs.wait_event(ev_out[i])                     # out_d[i] copied out by its previous D2H
+            with torch.cuda.stream(cs):
+                plans[b].compute(pcm_d[i], lens, rng.randbits2(nj), out=out_h[i] if mapped[0] else out_d[i],
+                                 **mix[b])
+                ev_done[i].record(cs)
             if mapped[0]:
-                ev_out[b].record(comp[b])
+                ev_out[i].record(cs)
                 return
-            s_outs[b].wait_event(ev_done[b])
-            with torch.cuda.stream(s_outs[b]):
-                out_h[b].copy_(out_d[b], non_blocking=True)
-                ev_out[b].record(s_outs[b])
+            so = s_outs[b % nd]
+            so.wait_event(ev_done[i])
+            with torch.cuda.stream(so):
+                out_h[i].copy_(out_d[i], non_blocking=True)
+                ev_out[i].record(so)
 
         def xstep():
-            if B == 1:
-                xbatch(it[0] & 1)
-                it[0] += 1
-            else:
-                for b in range(B):
-                    xbatch(b)
+            par = it[0] & 1
+            it[0] += 1
+            for b in range(B):
+                xbatch(b, 2 * b + par)
 
         el_x = timed_steps(xstep, args.steps, args.warmup, sync, dd, cpu_dev)
         mapped[0] = True
@@ -579,10 +579,9 @@ def main():
                                   "note": "features stored by the OLA kernel straight into pinned host memory "
                                           "(fdlp_mapped_ptr) instead of the D2H copy"},
                 "note": "every batch's PCM copied in from pinned host memory and its float32 features copied back "
-                        "every step (%s); not the headline (inputs resident in HBM)" %
-                        ("double-buffered on two copy streams" if B == 1 else
-                         "%d batches in flight on %d compute streams, one H2D stream, %d D2H stream(s)" %
-                         (B, nc, nd))}
+                        "every step (%d batch(es) in flight on %d compute stream(s), two device buffer sets per "
+                        "batch on alternate steps, one H2D stream, %d D2H stream(s)); not the headline (inputs "
+                        "resident in HBM)" % (B, len(comp), nd)}
 
     audio_h = world * args.steps * B * audio_s / 3600.0
     value = audio_h / elapsed

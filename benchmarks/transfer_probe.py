@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--seconds", type=float, default=4.0)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only-xstep", action="store_true", help="time only the double-buffered step (for traces)")
+    ap.add_argument("--split-probe", action="store_true",
+                    help="D2H / H2D rates with each copy split into K chunks on K streams (K = 1, 2, 4, 8), "
+                         "alone and with both directions at once")
     ap.add_argument("--d2h-variants", action="store_true",
                     help="device->host copy into differently allocated host buffers (hipMemcpyAsync): alone, "
                          "and overlapped with one compute step")
@@ -103,6 +106,37 @@ def main():
 
     nb_in = pin_in.numel() * pin_in.element_size()
     nb_out = out_d[0].numel() * 4
+    if a.split_probe:
+        res = {"sdma": os.environ.get("HSA_ENABLE_SDMA", "default")}
+        so = [torch.cuda.Stream(dev) for _ in range(8)]
+        si = [torch.cuda.Stream(dev) for _ in range(8)]
+        src_o, dst_o = out_d[1].view(-1), out_h[1].view(-1)
+        src_i, dst_i = pin_in.view(-1), pcm_d[1].view(-1)
+
+        def chunks(n, k):
+            step = (n + k - 1) // k
+            return [(i, min(n, i + step)) for i in range(0, n, step)]
+
+        for k in (1, 2, 4, 8):
+            def d2h_k():
+                for q, (lo, hi) in enumerate(chunks(src_o.numel(), k)):
+                    with torch.cuda.stream(so[q]):
+                        dst_o[lo:hi].copy_(src_o[lo:hi], non_blocking=True)
+
+            def h2d_k():
+                for q, (lo, hi) in enumerate(chunks(src_i.numel(), k)):
+                    with torch.cuda.stream(si[q]):
+                        dst_i[lo:hi].copy_(src_i[lo:hi], non_blocking=True)
+
+            def both_k():
+                h2d_k()
+                d2h_k()
+
+            t_o, t_i, t_b = timeit(d2h_k, a.reps), timeit(h2d_k, a.reps), timeit(both_k, a.reps)
+            res["k%d" % k] = {"d2h_GBps": round(nb_out / t_o / 1e9, 2), "h2d_GBps": round(nb_in / t_i / 1e9, 2),
+                              "both_GBps": round((nb_in + nb_out) / t_b / 1e9, 2)}
+        print(json.dumps(res))
+        return
     if a.d2h_variants:
         import ctypes
         hip = ctypes.CDLL("libamdhip64.so")
