@@ -571,7 +571,7 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
                                                                    const double* __restrict__ dense_rows,
                                                                    double scale2, double* __restrict__ dct) {
   using namespace dct1;
-  __shared__ double xch[kM];
+  __shared__ __attribute__((aligned(16))) double xch[kM];
   __shared__ double2 tab[kTabs + kC];  // tables + the (0, 0) task's X (pass 3)
   const int t = threadIdx.x;
   const int f = blockIdx.x;
@@ -676,11 +676,23 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
 #pragma unroll
   for (int j = 0; j < kC; ++j) y3[j].y = xch[a3 + j];
   // ---- pass 3: DFT_C over q3 -> X[k1 + A k2a + AB k2b]; unpack with X[M - k] ----
-  if (t >= 64 * ((kAB + 63) / 64)) return;  // whole waves without pass-3 tasks
-  rdft<kC>(y3);
+  // D leaves through LDS: the lanes' D[k] (k = lo + AB j: 8-byte pieces scattered over the row, 1.44x
+  // the row's bytes in partial-line writes, r03e PMC) are staged in xch, then every thread of the
+  // workgroup writes contiguous 16-byte pieces of the row; first D[0, M), then D[M, 2M) (held in
+  // registers meanwhile).  The waves without pass-3 tasks stay for the barriers and the row writes.
+  const bool task3 = t < kAB;
+  if (task3) rdft<kC>(y3);
   const int lo = k1 + kA * k2a;
-  const double2 rl = tab[kRtLo + lo], pl = tab[kPwLo + lo];
+  double2 rl = make_double2(0.0, 0.0), pl = rl;
+  if (task3) {
+    rl = tab[kRtLo + lo];
+    pl = tab[kPwLo + lo];
+  }
   double* drow = dct + (int64_t)f * N;
+  double dhi[kC];  // D[k + M] of the lane's k = lo + AB j
+#pragma unroll
+  for (int j = 0; j < kC; ++j) dhi[j] = 0.0;
+  __syncthreads();  // every lane's pass-3 reads of xch are done
   // D[k], D[k + M] from V = X_k and W = X_{M-k} (E / O split of the packed FFT, Makhoul post-twiddle)
   auto emit = [&](int j, double2 V, double2 W) {
     const double2 E = make_double2(0.5 * (V.x + W.x), 0.5 * (V.y - W.y));
@@ -692,14 +704,13 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
     const double2 tt = cmul(rt, O);
     const double2 V1 = make_double2(E.x + tt.x, E.y + tt.y);
     const double2 V2 = make_double2(E.x - tt.x, E.y - tt.y);
-    const int k = lo + kAB * j;
-    drow[k] = (w1.x * V1.x - w1.y * V1.y) * scale2;
-    drow[k + kM] = (w2.x * V2.x - w2.y * V2.y) * scale2;
+    xch[lo + kAB * j] = (w1.x * V1.x - w1.y * V1.y) * scale2;
+    dhi[j] = (w2.x * V2.x - w2.y * V2.y) * scale2;
   };
   // pairs in lanes (2i, 2i+1) and the self-paired (0, 12) (mode 2): X_{M-k} is register C-1-j of the
   // partner lane, or of the lane itself
-  const bool act = t < kAB && mode != 1;
-  if (mode == 1) {  // the one lane of task (0, 0) parks its X in LDS (read back by the same lane below)
+  const bool act = task3 && mode != 1;
+  if (task3 && mode == 1) {  // the one lane of task (0, 0) parks its X in LDS (read back by the same lane below)
 #pragma unroll
     for (int j = 0; j < kC; ++j) tab[kTabs + j] = y3[j];
   }
@@ -714,10 +725,22 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
       if (jm != j) emit(jm, b, mode == 2 ? a : sa);
     }
   }
-  if (mode == 1) {  // (0, 0): X_{M-k} = its own value (C - j) mod C, parked in LDS above
+  if (task3 && mode == 1) {  // (0, 0): X_{M-k} = its own value (C - j) mod C, parked in LDS above
 #pragma unroll
     for (int j = 0; j < kC; ++j) emit(j, tab[kTabs + j], tab[kTabs + (kC - j) % kC]);
   }
+  // row writes: 16-byte pieces, consecutive threads on consecutive pieces (M / 2 = 6000 per half)
+  double2* drow2 = reinterpret_cast<double2*>(drow);
+  const double2* xch2 = reinterpret_cast<const double2*>(xch);
+  __syncthreads();
+  for (int q = t; q < kM / 2; q += kThreads) drow2[q] = xch2[q];
+  __syncthreads();
+  if (task3) {
+#pragma unroll
+    for (int j = 0; j < kC; ++j) xch[lo + kAB * j] = dhi[j];
+  }
+  __syncthreads();
+  for (int q = t; q < kM / 2; q += kThreads) drow2[kM / 2 + q] = xch2[q];
 }
 
 // host tables of dct_frame_kernel (double2 [dct1::kTabs]); empty unless N = 24000 with the real FFT
