@@ -586,14 +586,16 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
     const bool fast = pcm_kind == 0 && fd.noise_off < 0 && t0 >= 0 && t0 + N <= fd.T;
     if (fast) {
       const int16_t* xs = (const int16_t*)pcm + fd.pcm_off + t0;
+      const double2* hwin = c.dct1_tw + kTabs;  // the window in Makhoul order (dct_frame_tables)
 #pragma unroll
       for (int q1 = 0; q1 < kA; ++q1) {
         const int q = kBC * q1 + t;
         // v[2q] = x[4q], v[2q+1] = x[4q+2] in the first half, mirrored (x[2N-1-4q], x[2N-3-4q]) after
         const int m0 = 4 * q1 < kA * 2 ? 4 * q : 2 * N - 1 - 4 * q;
         const int m1 = 4 * q1 < kA * 2 ? 4 * q + 2 : 2 * N - 3 - 4 * q;
-        y1[q1].x = __dmul_rn((double)xs[m0], c.hamming[m0]);
-        y1[q1].y = __dmul_rn((double)xs[m1], c.hamming[m1]);
+        const double2 hw = hwin[q];  // (hamming[m0], hamming[m1]): one coalesced 16-byte load
+        y1[q1].x = __dmul_rn((double)xs[m0], hw.x);
+        y1[q1].y = __dmul_rn((double)xs[m1], hw.y);
       }
     }
   }
@@ -744,11 +746,17 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
 }
 
 // host tables of dct_frame_kernel (double2 [dct1::kTabs]); empty unless N = 24000 with the real FFT
-std::vector<double2> dct_frame_tables(int N) {
+std::vector<double2> dct_frame_tables(int N, const std::vector<double>& window) {
   using namespace dct1;
   std::vector<double2> tab;
-  if (N != 2 * kM) return tab;
-  tab.resize(kTabs);
+  if (N != 2 * kM || (int)window.size() != N) return tab;
+  tab.resize(kTabs + kM);
+  // after the tables: the analysis window in the fast gather's order, (w[m0(q)], w[m1(q)]) for the packed
+  // sample q = v[2q] + i v[2q+1] (v = the Makhoul reorder), so pass 1 reads it coalesced
+  for (int q = 0; q < kM; ++q) {
+    const bool lo = q < kM / 2;
+    tab[kTabs + q] = make_double2(window[lo ? 4 * q : 2 * N - 1 - 4 * q], window[lo ? 4 * q + 2 : 2 * N - 3 - 4 * q]);
+  }
   const long double PI = 3.141592653589793238462643383279502884L;
   auto root = [&](long long e, long long n) {  // W_n^e = exp(-2 pi i e / n)
     const long double ang = -2.0L * PI * (long double)(e % n) / (long double)n;

@@ -121,7 +121,7 @@ hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const 
 hipError_t launch_dct_frame(const DevConsts& c, const void* pcm, int pcm_kind, const int16_t* noise,
                             const FrameDesc* frames, const double* dense_rows, int nframes, double* dct,
                             hipStream_t s);
-std::vector<double2> dct_frame_tables(int N);
+std::vector<double2> dct_frame_tables(int N, const std::vector<double>& window);
 hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* dense_rows,
                            int nframes_or_items, double* r, hipStream_t s);
 hipError_t launch_autocorr_structured(const DevConsts& c, const double* dct, int nframes, double* r,

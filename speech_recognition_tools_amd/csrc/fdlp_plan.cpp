@@ -728,7 +728,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   PLAN_TRY(upload(&p->d_om1, om1.data(), om1.size()));
   PLAN_TRY(upload(&p->d_om2, om2.data(), om2.size()));
   if (p->real_fft && !p->cplx) {  // the recipes' N = 24000: one DCT kernel per frame
-    const std::vector<double2> dct1 = fdlp::dct_frame_tables(N);
+    const std::vector<double2> dct1 = fdlp::dct_frame_tables(N, ham);
     if (!dct1.empty()) PLAN_TRY(upload(&p->d_dct1, dct1.data(), dct1.size()));
   }
 
