@@ -625,16 +625,20 @@ __device__ __forceinline__ void c8_relayout(const double (&A)[S], double (&An)[S
 #pragma unroll
   for (int j = 0; j < S; ++j) sc[li * S + j] = A[j];
   wave_lds_sync();
+  // positions outside [0, 8 S) are read unclamped and dropped by the select: m stays within
+  // [-16, 8 (S + 2)) c [-16, 8 SL8), inside the item's LDS area (8 doubles of gap and r_{kR-8..} below sc).
+  // Clamping them to sc[0] put those lanes on one bank beside the odd-stride lanes of the other items:
+  // 1.15e7 bank-conflict cycles per launch (r03e PMC).
 #pragma unroll
   for (int j = 0; j < S + 2; ++j) {
     const int m = li * (S + 2) + j;
-    const double v = sc[m < 8 * S ? m : 0];
+    const double v = sc[m];
     An[j] = m < 8 * S ? v : 0.0;
   }
 #pragma unroll
   for (int j = 0; j < S + 2; ++j) {
     const int m = 8 * S - 1 - li * (S + 2) - j;
-    const double v = sc[m >= 0 ? m : 0];
+    const double v = sc[m];
     Bn[j] = m >= 0 ? v : 0.0;
   }
 }
