@@ -363,6 +363,8 @@ def parse_args(argv=None):
     ap.add_argument("--xfer-compute-streams", type=int, default=0,
                     help="PCIe pass: compute streams for the batches in flight (0: one per batch)")
     ap.add_argument("--pipeline", type=int, default=None, help="sub-batches over two streams (plan default 1)")
+    ap.add_argument("--dct-path", default="auto", choices=["auto", "four_step"],
+                    help="DCT stage: auto (one dct_frame_kernel per frame at N = 24000) or the four-step pair")
     ap.add_argument("--inflight", type=int, default=4,
                     help="device batches in flight per GPU: independent plans on their own HIP streams, each "
                          "featurising its own batch every step (their kernels overlap on the device)")
@@ -475,6 +477,8 @@ def main():
     # signals rotated), and its own output buffer.
     B = max(1, args.inflight)
     plans = [plan] + [FdlpPlan(cfg, device=dev.index, max_frames=frames) for _ in range(B - 1)]
+    for pl in plans:
+        pl.set_dct_path(args.dct_path)
     shifts = [7919 * b for b in range(B)]
     pcms = [pcm] + [torch.roll(pcm, shifts[b]) for b in range(1, B)]
     outs = [out] + [torch.empty_like(out) for _ in range(B - 1)]
@@ -641,7 +645,7 @@ def main():
                        "U(1,30)" if args.workload == "librispeech" else "U(2,15)", audio_s / max(len(lens), 1)),
                    "frames_per_step_per_gpu": B * frames, "nfilters": cfg.nfilters, "order": cfg.order,
                    "coeff_num": cfg.coeff_num, "coeff_range": cfg.coeff_range, "fbank": cfg.fbank_type,
-                   "support_eps": cfg.support_eps, "autocorr_path": path,
+                   "support_eps": cfg.support_eps, "autocorr_path": path, "dct_path": plan.dct_path,
                    "add_noise": "babble,%g (on the device, in the timed kernels)" % NOISE_SNR
                    if noise_host is not None else "clean",
                    "reverb_sets": ("1ch T60 0.7 s / 8ch_beamformit T60 0.35 s, synthetic RIRs applied by "
