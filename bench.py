@@ -292,8 +292,9 @@ def autocorr_flops(plan, support):
     """Useful fp64 FLOPs of the autocorrelation stage per analysis frame (2 per MAC) for the
     algorithm the path runs.  direct: nlags MACs per tap of every band support (circular).
     structured_mfma: the two skirt sweeps, the per-band flat tops and the boundary straddles;
-    structured: the same with the flat tops as one sweep over [min m1, max m2) whose products run to N
-    (DESIGN.md "Structured autocorrelation")."""
+    structured: the same with the flat tops as one sweep over [min m1, max m2) whose products run to N,
+    and the wrap straddle shared by the bands with skirt taps at both edges (DESIGN.md "Structured
+    autocorrelation")."""
     nl, N = plan.nlags, plan.N
     lags = np.arange(nl)
     trunc = lambda n: float(np.maximum(n - lags, 0).sum())      # truncated autocorrelation
@@ -305,10 +306,17 @@ def autocorr_flops(plan, support):
     if path == "structured":
         pos = np.arange(int(m1.min()), int(m2.max()))
         macs += float(np.minimum(nl, N - pos).sum())
+    # structured: the wrap straddle of a band whose first / last nlags - 1 taps are skirt taps is one
+    # band-independent Wrap row per frame (ac_wrap_kernel) times sqrt(K_j K'_j): counted once per frame
+    shared = (m1 >= nl - 1) & (m2 <= N - (nl - 1)) if path == "structured" else np.zeros(plan.B, bool)
+    if shared.any():
+        macs += float(np.minimum(lags, nl - 1).sum())
     for j in range(plan.B):
         if path != "structured":
             macs += trunc(int(m2[j] - m1[j]))
         for b, lb in ((m1[j], 0), (m2[j], m1[j]), (N, m2[j])):
+            if b == N and shared[j]:
+                continue
             macs += float(np.minimum(lags, min(int(b - lb), nl - 1)).sum())
     return 2.0 * macs
 

@@ -33,6 +33,7 @@ namespace fdlp {
 constexpr int kAcChunk = 256;   // positions per staged chunk (4 k-steps)
 constexpr int kAcRing = 512;    // ring holds chunks c and c+1 (the window halo of c is <= 16*NT <= 256)
 constexpr int kAcPer = kAcChunk / 64;
+constexpr int kMaxWrapLags = 256;  // ac_wrap_kernel LDS edges (nlags <= 256)
 
 template <int NT>
 __global__ __launch_bounds__(64, 4) void autocorr_kernel(DevConsts c, const double* __restrict__ dct,
@@ -390,7 +391,8 @@ template <int NT, bool VS>
 __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const double* __restrict__ dct,
                                                         double* __restrict__ r, const double* __restrict__ rup,
                                                         const double* __restrict__ rflat,
-                                                        const double* __restrict__ rpart, int items) {
+                                                        const double* __restrict__ rpart,
+                                                        const double* __restrict__ rwrap, int items) {
   static_assert(16 * NT <= kAcChunk, "window halo must fit one chunk");
   constexpr int kEpi = (32 + 31) * 17;                   // diag_blocks<NT, 32> image
   constexpr int kWin = (16 * NT + 63) / 64 * 64;         // A window of a straddle (>= nlags - 1)
@@ -405,6 +407,8 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
   const int f = item / c.B, j = item % c.B;
   const int2 reg = c.sk_reg[j];
   const int m1 = reg.x, m2 = reg.y;
+  // the wrap straddle of a band whose first / last nlags - 1 taps are skirt taps is kw Wrap (ac_wrap_kernel)
+  const double kw = (VS && rwrap) ? c.sk_wrap[j] : 0.0;
   const double* drow = dct + (int64_t)f * N;
   const double* wrow = c.fbank + (int64_t)j * N;
   const int i_lane = lane & 15;
@@ -460,7 +464,7 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
   double* xa = xs;
   double* xb = xs + kWin;
 #pragma unroll 1
-  for (int e = 0; e < 3; ++e) {
+  for (int e = 0; e < (kw != 0.0 ? 2 : 3); ++e) {
     const int b = e == 0 ? m1 : (e == 1 ? m2 : N);
     int lb = e == 0 ? 0 : (e == 1 ? m1 : m2);
     lb = max(lb, b - (nlags - 1));
@@ -522,13 +526,15 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
     const double* fo = rflat + (int64_t)item * nlags;
     const int2 fb = c.fl_band[j];
     const int pmask = fb.y & ((1 << (c.fl_H - 1)) - 1);  // parts h < fl_H - 1 added in increasing h
-    double rv[kNB], uv[kNB], fv[kNB];
+    double rv[kNB], uv[kNB], fv[kNB], wv[kNB];
+    const double* wo = rwrap + (int64_t)f * nlags;
 #pragma unroll
     for (int g = 0; g < kNB; ++g) {
       const int L = min(32 * g + (lane >> 1), nlags - 1);  // clamped: the loads are unconditional
       rv[g] = ro[L];
       uv[g] = uo[L];
       fv[g] = fo[L];
+      wv[g] = kw != 0.0 ? wo[L] : 0.0;
     }
     if (pmask) {
       for (int rest = pmask; rest; rest &= rest - 1) {
@@ -540,10 +546,39 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
 #pragma unroll
     for (int g = 0; g < kNB; ++g) {
       const int L = 32 * g + (lane >> 1);
-      if ((lane & 1) == 0 && L < nlags) ro[L] = sums[g] + rv[g] + uv[g] + fv[g];
+      if ((lane & 1) == 0 && L < nlags) {
+        const double v = sums[g] + rv[g] + uv[g] + fv[g];
+        ro[L] = kw != 0.0 ? v + kw * wv[g] : v;
+      }
     }
   } else {
     diag_blocks<NT, 32>(acc, xs, nlags, lane, [&](int L, double v) { ro[L] = v + ro[L] + uo[L]; });
+  }
+}
+
+// Wrap straddle shared by the bands of a frame whose first / last nlags - 1 taps are skirt taps: there
+// x_j = sqrt(K_j) E D below m1_j and sqrt(K'_j) E' D above m2_j, so the pairs crossing the circular wrap
+// at N give sqrt(K_j K'_j) Wrap[l] with one band-independent
+//   Wrap[l] = sum_{i < l} z[N - l + i] y[i],   z = E' D (top nlags - 1 bins), y = E D (bottom ones)
+// (ac_band_kernel adds it in place of the band's own wrap straddle).  One wave per frame, a lane per lag
+// (l = lane, lane + 64, ...), the two edges staged in LDS, i ascending.
+__global__ __launch_bounds__(64) void ac_wrap_kernel(DevConsts c, const double* __restrict__ dct,
+                                                     double* __restrict__ rwrap, int nframes) {
+  __shared__ double zt[kMaxWrapLags], yh[kMaxWrapLags];
+  const int f = blockIdx.x;
+  if (f >= nframes) return;
+  const int N = c.N, nlags = c.nlags, L1 = nlags - 1;
+  const double* drow = dct + (int64_t)f * N;
+  for (int i = threadIdx.x; i < L1; i += 64) {
+    const int mt = N - L1 + i;
+    zt[i] = c.sk_e[N + mt] * drow[mt];
+    yh[i] = c.sk_e[i] * drow[i];
+  }
+  __syncthreads();
+  for (int l = threadIdx.x; l < nlags; l += 64) {
+    double acc = 0.0;
+    for (int i = 0; i < l; ++i) acc = fma(zt[L1 - l + i], yh[i], acc);
+    rwrap[(int64_t)f * nlags + l] = acc;
   }
 }
 
@@ -938,28 +973,30 @@ static hipError_t launch_vsweep(const DevConsts& c, const double* dct, int nfram
 
 template <int NT>
 static hipError_t launch_struct_nt(const DevConsts& c, const double* dct, int nframes, double* r, double* rup,
-                                   double* rflat, double* rpart, hipStream_t s) {
+                                   double* rflat, double* rpart, double* rwrap, hipStream_t s) {
   if (rflat) {  // lag-parallel VALU sweeps (flat tops included) + straddles
     const hipError_t e = launch_vsweep(c, dct, nframes, r, rup, rflat, rpart, s);
     if (e != hipSuccess) return e;
+    const bool wrap = rwrap && c.sk_wrap && c.nlags <= kMaxWrapLags;
+    if (wrap) hipLaunchKernelGGL(ac_wrap_kernel, dim3(nframes), dim3(64), 0, s, c, dct, rwrap, nframes);
     hipLaunchKernelGGL((ac_band_kernel<NT, true>), dim3(xcd_grid(nframes * c.B)), dim3(64), 0, s, c, dct, r, rup,
-                       rflat, rpart, nframes * c.B);
+                       rflat, rpart, wrap ? rwrap : nullptr, nframes * c.B);
     return hipGetLastError();
   }
   const size_t tab = sizeof(SkSnap) * (size_t)c.B;
   hipLaunchKernelGGL((ac_sweep_kernel<NT, 32>), dim3(xcd_grid(2 * nframes)), dim3(64), tab, s, c, dct, r, rup, 2 * nframes);
   hipLaunchKernelGGL((ac_band_kernel<NT, false>), dim3(xcd_grid(nframes * c.B)), dim3(64), 0, s, c, dct, r, rup,
-                     nullptr, nullptr, nframes * c.B);
+                     nullptr, nullptr, nullptr, nframes * c.B);
   return hipGetLastError();
 }
 
 hipError_t launch_autocorr_structured(const DevConsts& c, const double* dct, int nframes, double* r,
-                                      double* rup, double* rflat, double* rpart, hipStream_t s) {
+                                      double* rup, double* rflat, double* rpart, double* rwrap, hipStream_t s) {
   if (nframes <= 0) return hipSuccess;
   if (!c.sk_e || !c.sk_snap || !c.sk_reg) return hipErrorInvalidValue;
   if (rflat && (!c.fl_ev || !c.fl_band || (c.fl_H > 1 && !rpart))) return hipErrorInvalidValue;
   switch (autocorr_tiles(c.nlags)) {
-#define FDLP_ST_CASE(n) case n: return launch_struct_nt<n>(c, dct, nframes, r, rup, rflat, rpart, s);
+#define FDLP_ST_CASE(n) case n: return launch_struct_nt<n>(c, dct, nframes, r, rup, rflat, rpart, rwrap, s);
     FDLP_ST_CASE(1) FDLP_ST_CASE(2) FDLP_ST_CASE(3) FDLP_ST_CASE(4) FDLP_ST_CASE(5)
     FDLP_ST_CASE(6) FDLP_ST_CASE(7) FDLP_ST_CASE(8) FDLP_ST_CASE(9) FDLP_ST_CASE(10)
     FDLP_ST_CASE(11) FDLP_ST_CASE(12) FDLP_ST_CASE(13) FDLP_ST_CASE(14) FDLP_ST_CASE(15)

@@ -84,6 +84,9 @@ struct DevConsts {
   int fl_H = 1;
   int fl_part_lo[kMaxFlatParts] = {0}, fl_part_hi[kMaxFlatParts] = {0}, fl_part_ev[kMaxFlatParts + 1] = {0};
   const int2* fl_band = nullptr;  // [B] (chain, bitmask of the parts h < fl_H - 1 it needs a partial from)
+  // wrap straddle shared by the bands whose first / last nlags - 1 taps lie on their skirts: [B]
+  // sqrt(K_j K'_j), 0 for the bands whose wrap straddle ac_band_kernel computes from the taps; null: none
+  const double* sk_wrap = nullptr;
   // persistent LPC kernel: resident blocks on the plan's device (prepare_lpc_env, at plan creation)
   int lpc_blocks = 0;
   int lpc_mode = 0;        // fdlp_set_lpc_path: 0 lattice kernels (default), 1 the LDS Durbin (cross-check)
@@ -125,7 +128,7 @@ std::vector<double2> dct_frame_tables(int N, const std::vector<double>& window);
 hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* dense_rows,
                            int nframes_or_items, double* r, hipStream_t s);
 hipError_t launch_autocorr_structured(const DevConsts& c, const double* dct, int nframes, double* r,
-                                      double* rup, double* rflat, double* rflat_part, hipStream_t s);
+                                      double* rup, double* rflat, double* rflat_part, double* rwrap, hipStream_t s);
 int vsweep_lanes_lags(int nlags);   // lags per lane of ac_vsweep_kernel, 0 = unsupported
 int vsweep_chains(int C);           // chain count instantiated for C needed chains, 0 = unsupported
 hipError_t launch_levinson(const DevConsts& c, const double* r, int items, double* a,

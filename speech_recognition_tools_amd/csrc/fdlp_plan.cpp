@@ -150,6 +150,11 @@ struct SkirtTables {
   int fl_H = 1;
   int part_lo[fdlp::kMaxFlatParts] = {0}, part_hi[fdlp::kMaxFlatParts] = {0}, part_ev[fdlp::kMaxFlatParts + 1] = {0};
   std::vector<int2> fl_band;  // [B] (chain, partial-part mask)
+  // wrap straddle: band j whose last nlags-1 taps lie on its upper skirt and first nlags-1 on its lower
+  // skirt has straddle_N,j[l] = sqrt(K_j K'_j) Wrap[l], Wrap[l] = sum_{i<l} z[N-l+i] y[i] (one per frame);
+  // wrap_kw[j] = sqrt(K_j K'_j) for those bands, 0 for the others (ac_band_kernel computes theirs)
+  std::vector<double> wrap_kw;
+  bool wrap_any = false;
 };
 
 // Split the flat sweep [fl_lo, fl_hi) into H equal position parts (more waves: the flat sweep has one
@@ -267,6 +272,17 @@ bool skirt_tables(const fdlp_config& c, int B, int N, int nfft, SkirtTables* T) 
     K[j] = (double)powl(10.0L, ea);
     K[(size_t)B + j] = (double)powl(10.0L, eb);
   }
+  const int L1 = c.order + 1;  // nlags - 1: the longest straddle
+  T->wrap_kw.assign(B, 0.0);
+  T->wrap_any = false;
+  for (int j = 0; j < B; ++j) {
+    if (T->reg[j].x >= L1 && T->reg[j].y <= N - L1) {
+      const long double ea = (long double)a * ((long double)om - 2.0L * cf[j] + 2.0L * c0);
+      const long double eb = (long double)b * (2.0L * cf[j] + (long double)om - 2.0L * c0);
+      T->wrap_kw[j] = (double)powl(10.0L, 0.5L * (ea + eb));
+      T->wrap_any = true;
+    }
+  }
   T->snap.resize(2 * (size_t)B);
   for (int sk = 0; sk < 2; ++sk) {
     std::vector<fdlp::SkSnap> t(B);
@@ -372,6 +388,7 @@ struct fdlp_plan {
   bool vs_avail = false;             // lag-parallel VALU sweeps possible (flat chains, lag count)
   SkirtTables sk;
   double *d_sk_e = nullptr, *r_up = nullptr, *r_flat = nullptr, *r_flat_part = nullptr;
+  double *d_sk_wrap = nullptr, *r_wrap = nullptr;  // wrap-straddle factors [B] / per-frame Wrap rows [F, nlags]
   fdlp::FlatEv* d_fl_ev = nullptr;
   int2* d_fl_band = nullptr;
   fdlp::SkSnap* d_sk_snap = nullptr;
@@ -421,7 +438,8 @@ int free_plan(fdlp_plan* p) {
   void* devs[] = {p->d_fbank, p->d_hamming, p->d_weights, p->d_env_cos, p->d_env_win, p->d_tw1, p->d_post, p->d_rtw,
                   p->d_om1, p->d_om2, p->d_dct1, p->d_lo, p->d_hi, p->ws.z, p->ws.dct, p->ws.r, p->ws.a, p->ws.gg,
                   p->ws.cep, p->ws.env, p->ws.a_pad, p->d_frames, p->d_utts, p->d_sk_e, p->r_up, p->d_sk_snap,
-                  p->d_sk_reg, p->d_faxis, p->r_flat, p->d_fl_ev, p->r_flat_part, p->d_fl_band};
+                  p->d_sk_reg, p->d_faxis, p->r_flat, p->d_fl_ev, p->r_flat_part, p->d_fl_band, p->d_sk_wrap,
+                  p->r_wrap};
   for (void* d : devs)
     if (d) (void)hipFree(d);
   if (p->h_frames) (void)hipHostFree(p->h_frames);
@@ -751,6 +769,10 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
       d.fl_lo = p->sk.fl_lo; d.fl_hi = p->sk.fl_hi;
       PLAN_TRY(upload(&p->d_fl_band, p->sk.fl_band.data(), p->sk.fl_band.size()));
       d.fl_band = p->d_fl_band; d.fl_H = p->sk.fl_H;
+      if (p->sk.wrap_any) {
+        PLAN_TRY(upload(&p->d_sk_wrap, p->sk.wrap_kw.data(), p->sk.wrap_kw.size()));
+        d.sk_wrap = p->d_sk_wrap;
+      }
       for (int h = 0; h < fdlp::kMaxFlatParts; ++h) { d.fl_part_lo[h] = p->sk.part_lo[h]; d.fl_part_hi[h] = p->sk.part_hi[h]; }
       for (int h = 0; h <= fdlp::kMaxFlatParts; ++h) d.fl_part_ev[h] = p->sk.part_ev[h];
     }
@@ -773,6 +795,7 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
       hipMalloc((void**)&p->ws.env, sizeof(double) * items * p->kk) != hipSuccess ||
       (p->sk_avail && hipMalloc((void**)&p->r_up, sizeof(double) * items * p->nlags) != hipSuccess) ||
       (p->vs_avail && hipMalloc((void**)&p->r_flat, sizeof(double) * items * p->nlags) != hipSuccess) ||
+      (p->vs_avail && p->d_sk_wrap && hipMalloc((void**)&p->r_wrap, sizeof(double) * F * p->nlags) != hipSuccess) ||
       (p->vs_avail && p->sk.fl_H > 1 &&
        hipMalloc((void**)&p->r_flat_part, sizeof(double) * F * (p->sk.fl_H - 1) * fdlp::kMaxChains * p->nlags) !=
            hipSuccess) ||
@@ -980,7 +1003,9 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
       double* rpart = p->ac_path == FDLP_AC_STRUCTURED && p->r_flat_part
                           ? p->r_flat_part + (size_t)f0 * (p->sk.fl_H - 1) * fdlp::kMaxChains * nl
                           : nullptr;
-      HIP_TRY(fdlp::launch_autocorr_structured(p->dc, p->ws.dct + f0 * N, n, r, p->r_up + it0 * nl, rflat, rpart, st));
+      double* rwrap = p->ac_path == FDLP_AC_STRUCTURED && p->r_wrap ? p->r_wrap + (size_t)f0 * nl : nullptr;
+      HIP_TRY(fdlp::launch_autocorr_structured(p->dc, p->ws.dct + f0 * N, n, r, p->r_up + it0 * nl, rflat, rpart,
+                                               rwrap, st));
     } else {
       HIP_TRY(fdlp::launch_autocorr(p->dc, p->ws.dct + f0 * N, nullptr, its, r, st));
     }
