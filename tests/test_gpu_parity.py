@@ -158,6 +158,7 @@ STRUCT_CFGS = [
     ("cochlear,1,1,1,2.5,1", 7, 1.5, 238, 100),      # few wide bands, the largest order
     ("cochlear,0.02,1,1,2.5,1", 30, 0.5, 40, 40),    # (near-)empty flat tops
     ("cochlear,3,1,1,2.5,1", 60, 0.5, 20, 20),       # wide overlapping flat tops (many chains)
+    ("cochlear,1,0.05,1,0.05,1", 24, 1.0, 50, 50),   # shallow skirts: the shared wrap straddle carries weight
 ]
 
 
