@@ -607,15 +607,25 @@ __global__ __launch_bounds__(64) void ac_wrap_kernel(DevConsts c, const double* 
 //     128 prefetched into registers.
 // -----------------------------------------------------------------------------------------
 
-constexpr int kVsRing = 512;
 constexpr int kVsMirror = 16;
+#ifndef FDLP_VS_SKIRT3
+#define FDLP_VS_SKIRT3 0  // 1: skirt sweeps at three waves per SIMD (320-position ring, 128-position chunks, one
+                          // parked row; 137 VGPRs): measured 1.56 -> 2.19 ms (r03s), kept as a compile-time variant
+#endif
+// ring positions per unit (a power of two is not required: slots are taken modulo the ring) and the LDS
+// row stride; rows of 352 / 544 doubles keep each ds_read_b128 lane group on 64 distinct banks for the
+// 10-double lane stride of the window reads
+template <int C>
+constexpr int vs_ring() { return (C == 0 && FDLP_VS_SKIRT3) ? 320 : 512; }
+template <int C>
+constexpr int vs_row() { return (C == 0 && FDLP_VS_SKIRT3) ? 352 : 544; }
 // positions staged per chunk; the prefetch of the next chunk has to cover the HBM latency under load
 // (64 positions, ~3000 cycles of FMAs, measured too short).  The flat sweep keeps its chains in
 // registers, so it stages 128 at a time to stay at two waves per SIMD.
 template <int A, int C>
-constexpr int vs_chunk() { return (C == 0 && 18 * A < kVsRing - 256) ? 256 : 128; }
+constexpr int vs_chunk() { return (C == 0 && !FDLP_VS_SKIRT3 && 18 * A < vs_ring<C>() - 256) ? 256 : 128; }
 template <int C>
-constexpr int vs_waves_per_simd() { return 2; }
+constexpr int vs_waves_per_simd() { return (C == 0 && FDLP_VS_SKIRT3) ? 3 : 2; }
 
 template <int A, int V = 0>
 __device__ __forceinline__ void vs_bcast_all(double (&bb)[A], double cur) {
@@ -662,11 +672,24 @@ __global__ __launch_bounds__(64, vs_waves_per_simd<C>()) void ac_vsweep_kernel(D
   // snaps / fev (= c.sk_snap / c.fl_ev) as restrict parameters: not clobbered by the output stores,
   // so their wave-uniform reads become scalar loads
   constexpr int kVsChunk = vs_chunk<A, C>();
+  constexpr int kVsRing = vs_ring<C>();
+  constexpr int kRow = vs_row<C>();
   static_assert(A % 2 == 0 && A <= 16 && 18 * A < kVsRing - kVsChunk && A <= kVsMirror + 1, "vsweep geometry");
+  static_assert(kRow >= kVsRing + kVsMirror && kVsRing % 2 == 0, "ring row");
+  // slot of sweep position n (n >= -kVsRing): n mod kVsRing (a mask when the ring is a power of two)
+  auto slot_of = [](int n) {
+    if constexpr ((kVsRing & (kVsRing - 1)) == 0) return n & (kVsRing - 1);
+    else return (n + 8 * kVsRing) % kVsRing;
+  };
+  // wave-uniform base u (scalar modulo) plus a lane offset d < kVsRing
+  auto slot_add = [&](int u, int d) {
+    const int b = slot_of(__builtin_amdgcn_readfirstlane(u)) + d;
+    return b >= kVsRing ? b - kVsRing : b;
+  };
   // row stride 544 doubles = 17 x 256 B: each ds_read_b128 lane group (lanes 0-3,12-15 of one row and
   // 4-11 of the next, MI355X_MICROARCH.md LDS) then covers the 64 banks exactly with the 10-double lane
   // stride of the window reads (A = 10; a 528 stride measured 9.4e7 conflict cycles per launch)
-  __shared__ double ring_all[4][kVsRing + 32];
+  __shared__ double ring_all[4][kRow];
   static_assert(kVsMirror <= 32, "mirror fits the row padding");
   // C == 0: the two skirt sweeps, item = 2 group + skirt (a frame group's two sweeps adjacent on one
   // XCD, so its D rows are read from HBM once); C > 0: the flat-top sweep, item = group
@@ -732,7 +755,7 @@ __global__ __launch_bounds__(64, vs_waves_per_simd<C>()) void ac_vsweep_kernel(D
 #pragma unroll
     for (int q = 0; q < kPf; ++q) {
       const int n = base + 16 * q + l;
-      const int slot = n & (kVsRing - 1);
+      const int slot = slot_add(base, 16 * q + l);
       double v = pf[q];
       if constexpr (C == 0) v = pe[q] * v;
       v = (n >= 0 && n < N) ? v : 0.0;
@@ -756,7 +779,7 @@ __global__ __launch_bounds__(64, vs_waves_per_simd<C>()) void ac_vsweep_kernel(D
   // right after the ring commit and before the next prefetch.  A VMEM store's data registers must
   // not be rewritten before the store completes (vmcnt, in order with the prefetch loads), so storing
   // from reused registers would put a wait for the prefetch at the head of every block.
-  constexpr int P = C == 0 ? 2 : 1;
+  constexpr int P = (C == 0 && !FDLP_VS_SKIRT3) ? 2 : 1;
   double* const outb = kind == 0 ? rlow : (kind == 1 ? rup : rflat);
   double pend[P][A];
   int64_t prow[P];
@@ -850,10 +873,10 @@ __global__ __launch_bounds__(64, vs_waves_per_simd<C>()) void ac_vsweep_kernel(D
   // then the event is handled; usually a single unmasked pass
   auto block = [&](int n0, double (&lo)[A], const double (&hi)[A]) {
     ensure(n0);
-    const int base = (n0 + A * l) & (kVsRing - 1);
+    const int base = slot_add(n0, A * l);
 #pragma unroll
     for (int q = 0; q < A; ++q) lo[q] = rg[base + q];
-    const double cur = rg[(n0 + l) & (kVsRing - 1)];
+    const double cur = rg[slot_add(n0, l)];
     const int pos = n0 + l;
     int hi_m = min(n0 + A, nhi);
     for (;;) {
@@ -867,7 +890,7 @@ __global__ __launch_bounds__(64, vs_waves_per_simd<C>()) void ac_vsweep_kernel(D
 
   double X[A], Y[A];
   {
-    const int base = (A * b_top + A + A * l) & (kVsRing - 1);
+    const int base = slot_add(A * b_top + A, A * l);
 #pragma unroll
     for (int q = 0; q < A; ++q) Y[q] = rg[base + q];
   }
