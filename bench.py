@@ -353,6 +353,20 @@ def spawn_ranks(n, argv):
     return next((rc for rc in rcs if rc != 0), 0)
 
 
+def run_xfer_child(args):
+    """bench.py --xfer-only in a child process with GPU_MAX_HW_QUEUES = --xfer-hw-queues; its
+    with_transfers block, or None (with the child's tail on stderr) when it fails."""
+    argv = [a for a in sys.argv[1:] if a != "--xfer-only"] + ["--xfer-only", "--no-cpu-baseline"]
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(args.xfer_hw_queues))
+    p = subprocess.run([sys.executable, os.path.abspath(__file__)] + argv, env=env, capture_output=True, text=True)
+    lines = [l for l in p.stdout.strip().splitlines() if l.startswith("{")]
+    if p.returncode != 0 or not lines:
+        print("bench.py: PCIe-pass child failed (rc %d), measuring in-process:\n%s" % (p.returncode, p.stderr[-2000:]),
+              file=sys.stderr)
+        return None
+    return json.loads(lines[-1])["with_transfers"]
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -367,7 +381,12 @@ def parse_args(argv=None):
                     help="utterances per CPU-baseline process (default: about 10 s of oracle time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-transfers", action="store_true", help="skip the PCIe-inclusive timed pass")
-    ap.add_argument("--xfer-d2h-streams", type=int, default=1, help="PCIe pass: device-to-host copy streams")
+    ap.add_argument("--xfer-d2h-streams", type=int, default=2, help="PCIe pass: device-to-host copy streams")
+    ap.add_argument("--xfer-hw-queues", type=int, default=8,
+                    help="PCIe pass (N = 1): run it in a child process with GPU_MAX_HW_QUEUES set to this (the "
+                         "compute, H2D and D2H streams then get hardware queues of their own; 0: in-process, with "
+                         "the process default of 4)")
+    ap.add_argument("--xfer-only", action="store_true", help=argparse.SUPPRESS)  # the PCIe-pass child
     ap.add_argument("--xfer-compute-streams", type=int, default=0,
                     help="PCIe pass: compute streams for the batches in flight (0: one per batch)")
     ap.add_argument("--pipeline", type=int, default=None, help="sub-batches over two streams (plan default 1)")
@@ -424,6 +443,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
         per = args.cpu_per_worker or (10 if args.config == "reverb" else 24)
         cpu = cpu_baseline(args.config, [t for _, t, _ in mine], args.cpu_workers, per, noise_host)
+
+    # PCIe-inclusive pass of a single-GPU run in a child process (before this process touches the GPU):
+    # GPU_MAX_HW_QUEUES is read once per process, and the headline keeps the process default
+    xfer_child = None
+    if (world == 1 and not args.no_transfers and not args.dry_run and not args.xfer_only
+            and args.xfer_hw_queues > 0):
+        xfer_child = run_xfer_child(args)
 
     if world > 1:  # host-side rendezvous: the only cross-rank traffic is a barrier and a max (no RCCL)
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -511,17 +537,22 @@ def main():
 
     # 1) headline: device-resident input and output, no profiling events.  warmup, barrier + sync,
     #    exactly K steps, sync + barrier, max over ranks (speech_recognition_tools_amd.shard)
-    elapsed = timed_steps(step_inflight, args.steps, args.warmup, sync, dd, cpu_dev)
+    if args.xfer_only:
+        elapsed = elapsed_one = elapsed_prof = None
+    else:
+        elapsed = timed_steps(step_inflight, args.steps, args.warmup, sync, dd, cpu_dev)
 
     # 1b) one batch in flight (the same steps with B = 1), reported beside the headline
-    elapsed_one = timed_steps(step, args.steps, 1, sync, dd, cpu_dev) if B > 1 else elapsed
+    if not args.xfer_only:
+        elapsed_one = timed_steps(step, args.steps, 1, sync, dd, cpu_dev) if B > 1 else elapsed
 
     # 2) one batch per step with per-stage HIP events on the stream the kernels run on (roofline: the
     #    kernels alone, not overlapped with another batch's)
-    plan.set_profiling(True)
-    elapsed_prof = timed_steps(step, args.steps, 0, sync, dd, cpu_dev)
-    stages, ncalls = plan.stage_times()
-    plan.set_profiling(False)
+    if not args.xfer_only:
+        plan.set_profiling(True)
+        elapsed_prof = timed_steps(step, args.steps, 0, sync, dd, cpu_dev)
+        stages, ncalls = plan.stage_times()
+        plan.set_profiling(False)
 
     # 3) PCIe-inclusive: PCM copied in from pinned host memory and float32 features back to pinned host
     #    memory, every batch of every step.  Every batch in flight has two device buffer sets used on
@@ -531,8 +562,8 @@ def main():
     #    and one D2H stream (--xfer-d2h-streams); the compute of batch b stays on its own stream.
     #    `mapped` = the OLA kernel stores the features straight into the pinned host buffer through its
     #    device mapping instead of a D2H copy (measured slower: reported, not used).
-    xfer = None
-    if not args.no_transfers:
+    xfer = xfer_child
+    if not args.no_transfers and xfer_child is None:
         pin_in = torch.from_numpy(pcm_host).pin_memory()
         NB = 2 * B                                       # device buffer sets: (batch, step parity)
         pcm_d = [pcms[i // 2] if i % 2 == 0 else torch.empty_like(pcm) for i in range(NB)]
@@ -595,6 +626,10 @@ def main():
                         "batch on alternate steps, one H2D stream, %d D2H stream(s)); not the headline (inputs "
                         "resident in HBM)" % (B, len(comp), nd)}
 
+    if args.xfer_only:
+        xfer["hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES", "default")
+        print(json.dumps({"with_transfers": xfer}))
+        return
     audio_h = world * args.steps * B * audio_s / 3600.0
     value = audio_h / elapsed
     ms_step = elapsed / args.steps * 1e3
