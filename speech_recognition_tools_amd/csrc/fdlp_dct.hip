@@ -565,6 +565,9 @@ __device__ __forceinline__ void pass3_task(int t, int& k1, int& k2a, int& mode) 
 }
 }  // namespace dct1
 
+#ifndef FDLP_DCT_PHASES
+#define FDLP_DCT_PHASES 0  // 1: timing build only - thread 0 overwrites D[f][0..7] with phase timestamps
+#endif
 __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, const void* __restrict__ pcm,
                                                                    int pcm_kind, const int16_t* __restrict__ noise,
                                                                    const FrameDesc* __restrict__ frames,
@@ -576,6 +579,10 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
   const int t = threadIdx.x;
   const int f = blockIdx.x;
   constexpr int N = 2 * kM;
+#if FDLP_DCT_PHASES
+  long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (t == 0) ts[0] = wall_clock64();
+#endif
   for (int q = t; q < kTabs; q += kThreads) tab[q] = c.dct1_tw[q];
 
   // ---- pass 1: thread n2 = C q2 + q3 gathers z[BC q1 + n2] = v[2q] + i v[2q+1] (Makhoul order) ----
@@ -626,6 +633,9 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
   }
   if (t < kBC) rdft<kA>(y1);
   __syncthreads();  // tables
+#if FDLP_DCT_PHASES
+  if (threadIdx.x == 0) ts[1] = wall_clock64();
+#endif
   if (t < kBC) {
 #pragma unroll
     for (int k1 = 1; k1 < kA; ++k1) {  // W_M^{k1 n2}, k1 n2 = BC a + b: W_A^a W_M^b
@@ -653,12 +663,18 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
     __syncthreads();
   }
   // ---- pass 2: DFT_B over q2, twiddle W_BC^{k2a q3}; exchange 2: [k2a][k1][q3] ----
+#if FDLP_DCT_PHASES
+  if (threadIdx.x == 0) ts[2] = wall_clock64();
+#endif
   if (t < kAC) {
     rdft<kB>(y2);
 #pragma unroll
     for (int k2a = 1; k2a < kB; ++k2a) y2[k2a] = cmul(y2[k2a], tab[kTwBC + k2a * q3]);
   }
   int k1, k2a, mode;
+#if FDLP_DCT_PHASES
+  if (threadIdx.x == 0) ts[3] = wall_clock64();
+#endif
   dct1::pass3_task(t < kAB ? t : 0, k1, k2a, mode);
   double2 y3[kC];
   const int a3 = k2a * kAC + k1 * kC;
@@ -684,6 +700,9 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
   // registers meanwhile).  The waves without pass-3 tasks stay for the barriers and the row writes.
   const bool task3 = t < kAB;
   if (task3) rdft<kC>(y3);
+#if FDLP_DCT_PHASES
+  if (threadIdx.x == 0) ts[4] = wall_clock64();
+#endif
   const int lo = k1 + kA * k2a;
   double2 rl = make_double2(0.0, 0.0), pl = rl;
   if (task3) {
@@ -735,6 +754,9 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
   double2* drow2 = reinterpret_cast<double2*>(drow);
   const double2* xch2 = reinterpret_cast<const double2*>(xch);
   __syncthreads();
+#if FDLP_DCT_PHASES
+  if (threadIdx.x == 0) ts[5] = wall_clock64();
+#endif
   for (int q = t; q < kM / 2; q += kThreads) drow2[q] = xch2[q];
   __syncthreads();
   if (task3) {
@@ -743,6 +765,13 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
   }
   __syncthreads();
   for (int q = t; q < kM / 2; q += kThreads) drow2[kM / 2 + q] = xch2[q];
+#if FDLP_DCT_PHASES
+  __syncthreads();
+  if (t == 0) {
+    ts[6] = wall_clock64();
+    for (int i = 0; i < 7; ++i) drow[i] = (double)ts[i];
+  }
+#endif
 }
 
 // host tables of dct_frame_kernel (double2 [dct1::kTabs]); empty unless N = 24000 with the real FFT
