@@ -43,8 +43,8 @@ def main():
     d = plan.debug_fetch(F * n, keys=("dct",))["dct"][:, :7]
     ts = d.astype(np.int64)
     dur = np.diff(ts, axis=1) * 10.0  # ns
-    names = ["tables+gather+radix20", "twiddle+exchange1", "radix24+twiddle", "exchange2", "radix25",
-             "unpack+D rows"]
+    names = ["descriptor+gather+tables+radix20", "twiddle1+exchange1", "radix24+twiddle2", "exchange2+radix25",
+             "unpack+post-twiddle", "D rows out"]
     t0, t1 = ts[:, 0].min(), ts[:, 6].max()
     res = {"frames": int(ts.shape[0]), "kernel_span_us": (t1 - t0) / 100.0,
            "frame_us_mean": float((ts[:, 6] - ts[:, 0]).mean()) / 100.0,
