@@ -54,18 +54,59 @@ __global__ __launch_bounds__(64, 2) void k(const double* in, double* out, int it
   out[blockIdx.x * 64 + threadIdx.x] = s;
 }
 
+// ldspf: as lds, but each block's window (and broadcast source) is read one block ahead into a third
+// register bank, so the wait at a block head is for reads issued a whole block earlier
+__global__ __launch_bounds__(64, 2) void kpf(const double* in, double* out, int iters) {
+  __shared__ double ring[4][528];
+  const int l = threadIdx.x & 15, row = threadIdx.x >> 4;
+  for (int q = l; q < 528; q += 16) ring[row][q] = in[(q + row) & 255] + 1e-3 * q;
+  __syncthreads();
+  double acc[A], B0[A], B1[A], B2[A], bb[A];
+  for (int u = 0; u < A; ++u) { acc[u] = 0; B0[u] = in[u + l]; B2[u] = in[u + 20 + l]; bb[u] = in[u + 40]; }
+  double cur = in[l], curn;
+  auto rd = [&](double (&dst)[A], double& c, int n0) {
+    const int base = (n0 + A * l) & 510;
+#pragma unroll
+    for (int q = 0; q < A; ++q) dst[q] = ring[row][base + q];
+    c = ring[row][(n0 + l) & 511];
+  };
+  for (int it = 0; it < iters; it += 3) {
+    const int n0 = (it * A) & 511;
+    rd(B1, curn, n0 + A);
+    bcast_all(bb, cur);
+    block(acc, bb, B0, B2);
+    cur = curn;
+    rd(B2, curn, n0 + 2 * A);
+    bcast_all(bb, cur);
+    block(acc, bb, B1, B0);
+    cur = curn;
+    rd(B0, curn, n0 + 3 * A);
+    bcast_all(bb, cur);
+    block(acc, bb, B2, B1);
+    cur = curn;
+  }
+  double s = 0;
+  for (int u = 0; u < A; ++u) s += acc[u];
+  out[blockIdx.x * 64 + threadIdx.x] = s;
+}
+
+template <int MODE>
+static void launch(dim3 g, const double* in, double* out, int iters) {
+  if constexpr (MODE == 3) hipLaunchKernelGGL(kpf, g, dim3(64), 0, 0, in, out, iters);
+  else hipLaunchKernelGGL(k<MODE>, g, dim3(64), 0, 0, in, out, iters);
+}
 template <int MODE>
 static void run(const char* name, const double* in, double* out, int waves, int iters) {
   hipEvent_t a, b;
   hipEventCreate(&a); hipEventCreate(&b);
-  hipLaunchKernelGGL(k<MODE>, dim3(waves), dim3(64), 0, 0, in, out, 10);
+  launch<MODE>(dim3(waves), in, out, 10);
   hipEventRecord(a);
-  hipLaunchKernelGGL(k<MODE>, dim3(waves), dim3(64), 0, 0, in, out, iters);
+  launch<MODE>(dim3(waves), in, out, iters);
   hipEventRecord(b);
   hipEventSynchronize(b);
   float ms = 0;
   hipEventElapsedTime(&ms, a, b);
-  const double flops = 2.0 * 2 * A * A * 64.0 * waves * (double)iters;
+  const double flops = (MODE == 3 ? 1.0 : 2.0) * 2 * A * A * 64.0 * waves * (double)iters;  // kpf: one block per it
   printf("%-6s waves %5d  %.3f ms  %.1f TFLOP/s\n", name, waves, ms, flops / ms / 1e9);
 }
 
@@ -80,6 +121,7 @@ int main() {
     run<0>("fma", in, out, waves, 20000);
     run<1>("dpp", in, out, waves, 20000);
     run<2>("lds", in, out, waves, 20000);
+    run<3>("ldspf", in, out, waves, 40002);
   }
   return 0;
 }
