@@ -381,7 +381,9 @@ def parse_args(argv=None):
                     help="utterances per CPU-baseline process (default: about 10 s of oracle time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-transfers", action="store_true", help="skip the PCIe-inclusive timed pass")
-    ap.add_argument("--xfer-d2h-streams", type=int, default=2, help="PCIe pass: device-to-host copy streams")
+    ap.add_argument("--xfer-d2h-streams", type=int, default=0,
+                    help="PCIe pass: device-to-host copy streams (0: two in the child process that has its own "
+                         "hardware queues, one in-process, where more streams share queues with the kernels)")
     ap.add_argument("--xfer-hw-queues", type=int, default=8,
                     help="PCIe pass (N = 1): run it in a child process with GPU_MAX_HW_QUEUES set to this (the "
                          "compute, H2D and D2H streams then get hardware queues of their own; 0: in-process, with "
@@ -572,7 +574,7 @@ def main():
         # streams: H2D, D2H (--xfer-d2h-streams, batch b on b mod that) and compute (--xfer-compute-streams,
         # default one per batch in flight)
         s_in = torch.cuda.Stream(dev)
-        nd = max(1, args.xfer_d2h_streams)
+        nd = args.xfer_d2h_streams or (2 if args.xfer_only else 1)
         s_outs = [torch.cuda.Stream(dev) for _ in range(nd)]
         nc = args.xfer_compute_streams or B
         comp = [torch.cuda.current_stream(dev)] if B == 1 else [streams[b % nc] for b in range(B)]
