@@ -1147,12 +1147,15 @@ int lpc_env_region(int p, int M) {
 
 // Lattice-kernel instantiation of a plan: calls fn(integral_constant<SL>, integral_constant<CB>) or
 // returns hipErrorNotSupported when the plan runs the LDS Durbin (lpc_env_kernel).
+#ifndef FDLP_CEP_SB_ALWAYS
+#define FDLP_CEP_SB_ALWAYS 0  // 1: the super-block cepstrum (CB < 0) also for M <= 112 (A/B builds)
+#endif
 template <class Fn>
 static hipError_t lattice_dispatch_sl(const DevConsts& c, Fn&& fn) {
   using std::integral_constant;
   const int SL = (c.p + 1 + 15) / 16;
   if (SL > 16 || c.lpc_mode == 1) return hipErrorNotSupported;
-  if (c.M <= 16 * 7 && SL >= 9 && SL <= 11) {  // register-broadcast cepstrum (recipes: p 150, M 100)
+  if (!FDLP_CEP_SB_ALWAYS && c.M <= 16 * 7 && SL >= 9 && SL <= 11) {  // register-broadcast cepstrum (recipes: p 150, M 100)
     switch (SL) {
       case 9: return fn(integral_constant<int, 9>{}, integral_constant<int, 7>{});
       case 10: return fn(integral_constant<int, 10>{}, integral_constant<int, 7>{});
@@ -1160,7 +1163,7 @@ static hipError_t lattice_dispatch_sl(const DevConsts& c, Fn&& fn) {
       default: break;
     }
   }
-  if (c.M > 16 * 7 && SL >= 9 && SL <= 11) {  // the same over a sliding window (REVERB: M 450)
+  if ((FDLP_CEP_SB_ALWAYS || c.M > 16 * 7) && SL >= 9 && SL <= 11) {  // the same over a sliding window (REVERB: M 450)
     switch (SL) {
       case 9: return fn(integral_constant<int, 9>{}, integral_constant<int, -1>{});
       case 10: return fn(integral_constant<int, 10>{}, integral_constant<int, -1>{});
