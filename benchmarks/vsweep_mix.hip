@@ -90,9 +90,49 @@ __global__ __launch_bounds__(64, 2) void kpf(const double* in, double* out, int 
   out[blockIdx.x * 64 + threadIdx.x] = s;
 }
 
+// dppwin: the window moves one lane down per block by DPP (row_shr:1, two v_mov_b32_dpp per double); only
+// lane 0 of each row reads its 10 new values (and the broadcast source) from the LDS ring
+template <int SH = 0>
+__device__ __forceinline__ void shift_in(double (&dst)[A], const double (&src)[A], const double (&nv)[A]) {
+#pragma unroll
+  for (int q = 0; q < A; ++q) dst[q] = __builtin_amdgcn_update_dpp(nv[q], src[q], 0x111, 0xF, 0xF, false);
+}
+__global__ __launch_bounds__(64, 2) void kdw(const double* in, double* out, int iters) {
+  __shared__ double ring[4][528];
+  const int l = threadIdx.x & 15, row = threadIdx.x >> 4;
+  for (int q = l; q < 528; q += 16) ring[row][q] = in[(q + row) & 255] + 1e-3 * q;
+  __syncthreads();
+  double acc[A], X[A], Y[A], bb[A], nv[A];
+  for (int u = 0; u < A; ++u) { acc[u] = 0; X[u] = in[u + l]; Y[u] = in[u + 20 + l]; bb[u] = in[u + 40]; nv[u] = 0; }
+  double cur = in[l];
+  for (int it = 0; it < iters; ++it) {
+    const int n0 = (it * 2 * A) & 511;
+    if (l == 0) {
+#pragma unroll
+      for (int q = 0; q < A; ++q) nv[q] = ring[row][(n0 + q) & 510];
+    }
+    cur = ring[row][(n0 + l) & 511];
+    shift_in(Y, X, nv);  // new lo (Y) from the old lo (X) of the lane below; X becomes hi
+    bcast_all(bb, cur);
+    block(acc, bb, Y, X);
+    if (l == 0) {
+#pragma unroll
+      for (int q = 0; q < A; ++q) nv[q] = ring[row][(n0 + A + q) & 510];
+    }
+    cur = ring[row][(n0 + A + l) & 511];
+    shift_in(X, Y, nv);
+    bcast_all(bb, cur);
+    block(acc, bb, X, Y);
+  }
+  double s = 0;
+  for (int u = 0; u < A; ++u) s += acc[u];
+  out[blockIdx.x * 64 + threadIdx.x] = s;
+}
+
 template <int MODE>
 static void launch(dim3 g, const double* in, double* out, int iters) {
-  if constexpr (MODE == 3) hipLaunchKernelGGL(kpf, g, dim3(64), 0, 0, in, out, iters);
+  if constexpr (MODE == 4) hipLaunchKernelGGL(kdw, g, dim3(64), 0, 0, in, out, iters);
+  else if constexpr (MODE == 3) hipLaunchKernelGGL(kpf, g, dim3(64), 0, 0, in, out, iters);
   else hipLaunchKernelGGL(k<MODE>, g, dim3(64), 0, 0, in, out, iters);
 }
 template <int MODE>
@@ -122,6 +162,7 @@ int main() {
     run<1>("dpp", in, out, waves, 20000);
     run<2>("lds", in, out, waves, 20000);
     run<3>("ldspf", in, out, waves, 40002);
+    run<4>("dppwin", in, out, waves, 20000);
   }
   return 0;
 }
