@@ -583,7 +583,6 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
   long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (t == 0) ts[0] = wall_clock64();
 #endif
-  for (int q = t; q < kTabs; q += kThreads) tab[q] = c.dct1_tw[q];
 
   // ---- pass 1: thread n2 = C q2 + q3 gathers z[BC q1 + n2] = v[2q] + i v[2q+1] (Makhoul order) ----
   double2 y1[kA];
@@ -631,6 +630,8 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
       __syncthreads();
     }
   }
+  // the tables after the sample gather: their loads overlap the gather's instead of preceding them
+  for (int q = t; q < kTabs; q += kThreads) tab[q] = c.dct1_tw[q];
   if (t < kBC) rdft<kA>(y1);
   __syncthreads();  // tables
 #if FDLP_DCT_PHASES
