@@ -358,7 +358,12 @@ def run_xfer_child(args):
     with_transfers block, or None (with the child's tail on stderr) when it fails."""
     argv = [a for a in sys.argv[1:] if a != "--xfer-only"] + ["--xfer-only", "--no-cpu-baseline"]
     env = dict(os.environ, GPU_MAX_HW_QUEUES=str(args.xfer_hw_queues))
-    p = subprocess.run([sys.executable, os.path.abspath(__file__)] + argv, env=env, capture_output=True, text=True)
+    try:
+        p = subprocess.run([sys.executable, os.path.abspath(__file__)] + argv, env=env, capture_output=True,
+                           text=True, timeout=900)
+    except subprocess.TimeoutExpired:
+        print("bench.py: PCIe-pass child timed out, measuring in-process", file=sys.stderr)
+        return None
     lines = [l for l in p.stdout.strip().splitlines() if l.startswith("{")]
     if p.returncode != 0 or not lines:
         print("bench.py: PCIe-pass child failed (rc %d), measuring in-process:\n%s" % (p.returncode, p.stderr[-2000:]),
