@@ -208,7 +208,11 @@ def _latest_pmc(config="wsj"):
     """The newest committed PMC summary of a config (profiles/rNN*_pmc.json for wsj,
     profiles/rNN*_<config>_pmc.json otherwise; written by scripts/round_evidence.sh)."""
     import glob
-    c = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc.json")))
+
+    def order(f):  # rNN<letters>: round, then a..z before aa..zz (the evidence tags of a round)
+        tag = os.path.basename(f).split("_")[0]
+        return int(tag[1:3]), len(tag[3:]), tag[3:]
+    c = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc.json")), key=order)
     tagged = lambda f: any(("_%s_pmc" % k) in os.path.basename(f) for k in ("reverb", "chime4", "librispeech"))
     c = [f for f in c if ((("_%s_pmc" % config) in os.path.basename(f)) if config != "wsj" else not tagged(f))]
     return c[-1] if c else None
@@ -217,7 +221,7 @@ def _latest_pmc(config="wsj"):
 PMC_FILE = _latest_pmc()
 # kernels of each timed stage (fdlp_stage_times), as rocprofv3 names them
 STAGE_KERNELS = {"dct": ("fdlp::dct_frame", "fdlp::frames_dft1", "fdlp::dft2_dct"),
-                 "autocorr": {"structured": ("fdlp::ac_vsweep_kernel", "fdlp::ac_band_kernel"),
+                 "autocorr": {"structured": ("fdlp::ac_vsweep_kernel", "fdlp::ac_wrap_kernel", "fdlp::ac_band_kernel"),
                               "structured_mfma": ("fdlp::ac_sweep_kernel", "fdlp::ac_band_kernel"),
                               "direct": ("fdlp::autocorr_kernel",)},
                  "lpc_env": ("fdlp::durbin8_kernel", "fdlp::lpc_env_lattice_kernel", "fdlp::cep_kernel",
@@ -263,10 +267,12 @@ def step_pmc_bytes(pmc_file=None):
     return sum(tot) if tot else None
 
 
-STAGE_DESC = {"dct": "DCT stage: frames_dft1 + dft2_dct (four-step Makhoul DCT-II, fp64 VALU)",
+STAGE_DESC = {"dct": "DCT stage: dct_frame_kernel (one workgroup per frame, Makhoul DCT-II over a 20x24x25 "
+                     "in-register FFT, fp64 VALU; frames_dft1 + dft2_dct with --dct-path four_step)",
               "autocorr": {"structured": "autocorr stage: ac_vsweep_kernel x2 (fp64 VALU FMA, lag-parallel sweeps) + "
-                                         "ac_band_kernel (v_mfma_f64_16x16x4f64 straddles); the 78.6 TFLOP/s fp64 "
-                                         "peak is shared by the VALU and matrix pipes",
+                                         "ac_wrap_kernel (the wrap straddle shared by the bands) + ac_band_kernel "
+                                         "(v_mfma_f64_16x16x4f64 straddles); the 78.6 TFLOP/s fp64 peak is shared "
+                                         "by the VALU and matrix pipes",
                            "structured_mfma": "autocorr stage: ac_sweep_kernel + ac_band_kernel (v_mfma_f64_16x16x4f64)",
                            "direct": "autocorr stage: autocorr_kernel (v_mfma_f64_16x16x4f64)"},
               "lpc_env": "LPC stage: durbin8_kernel (Levinson-Durbin) + cepstrum + envelope kernels (fp64)",
