@@ -714,28 +714,40 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
   double dhi[kC];  // D[k + M] of the lane's k = lo + AB j
 #pragma unroll
   for (int j = 0; j < kC; ++j) dhi[j] = 0.0;
-  __syncthreads();  // every lane's pass-3 reads of xch are done
+  // the one lane of task (0, 0) pairs X_k with its own X_{M-k} (register (C - j) mod C): it parks its X
+  // in LDS, and 25 lanes of an otherwise idle wave (t = 512 ..) emit one output pair each (done by that
+  // lane alone, its 25 outputs ran after everyone else's while the workgroup waited at the barrier)
+  if (task3 && mode == 1) {
+#pragma unroll
+    for (int j = 0; j < kC; ++j) tab[kTabs + j] = y3[j];
+  }
+  const int hj = t - 8 * 64;
+  const bool helper = hj >= 0 && hj < kC;
+  static_assert(kThreads >= 8 * 64 + kC && kAB <= 8 * 64, "helper lanes of task (0, 0)");
+  __syncthreads();  // every lane's pass-3 reads of xch are done; the (0, 0) values are parked
   // D[k], D[k + M] from V = X_k and W = X_{M-k} (E / O split of the packed FFT, Makhoul post-twiddle)
-  auto emit = [&](int j, double2 V, double2 W) {
+  auto emit_pair = [&](int j, double2 V, double2 W, double2 rlo, double2 plo, double& d1, double& d2) {
     const double2 E = make_double2(0.5 * (V.x + W.x), 0.5 * (V.y - W.y));
     const double2 O = make_double2(0.5 * (V.y + W.y), -0.5 * (V.x - W.x));
-    const double2 rt = cmul(rl, tab[kRtHi + j]);
-    const double2 w1 = cmul(pl, tab[kPwHi + j]);
+    const double2 rt = cmul(rlo, tab[kRtHi + j]);
+    const double2 w1 = cmul(plo, tab[kPwHi + j]);
     constexpr double hr = 0.70710678118654752440;  // post[k + M] = post[k] e^{-i pi / 4}
     const double2 w2 = make_double2(hr * (w1.x + w1.y), hr * (w1.y - w1.x));
     const double2 tt = cmul(rt, O);
     const double2 V1 = make_double2(E.x + tt.x, E.y + tt.y);
     const double2 V2 = make_double2(E.x - tt.x, E.y - tt.y);
-    xch[lo + kAB * j] = (w1.x * V1.x - w1.y * V1.y) * scale2;
-    dhi[j] = (w2.x * V2.x - w2.y * V2.y) * scale2;
+    d1 = (w1.x * V1.x - w1.y * V1.y) * scale2;
+    d2 = (w2.x * V2.x - w2.y * V2.y) * scale2;
+  };
+  auto emit = [&](int j, double2 V, double2 W) {
+    double d1, d2;
+    emit_pair(j, V, W, rl, pl, d1, d2);
+    xch[lo + kAB * j] = d1;
+    dhi[j] = d2;
   };
   // pairs in lanes (2i, 2i+1) and the self-paired (0, 12) (mode 2): X_{M-k} is register C-1-j of the
   // partner lane, or of the lane itself
   const bool act = task3 && mode != 1;
-  if (task3 && mode == 1) {  // the one lane of task (0, 0) parks its X in LDS (read back by the same lane below)
-#pragma unroll
-    for (int j = 0; j < kC; ++j) tab[kTabs + j] = y3[j];
-  }
   // j and C-1-j together, so both registers are dead after the pair (C odd: the middle one alone)
 #pragma unroll
   for (int j = 0; j < (kC + 1) / 2; ++j) {
@@ -747,9 +759,11 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
       if (jm != j) emit(jm, b, mode == 2 ? a : sa);
     }
   }
-  if (task3 && mode == 1) {  // (0, 0): X_{M-k} = its own value (C - j) mod C, parked in LDS above
-#pragma unroll
-    for (int j = 0; j < kC; ++j) emit(j, tab[kTabs + j], tab[kTabs + (kC - j) % kC]);
+  double dh_help = 0.0;
+  if (helper) {  // task (0, 0), output pair hj: X_{AB hj} and X_{M - AB hj} = X_{AB ((C - hj) mod C)}
+    double d1;
+    emit_pair(hj, tab[kTabs + hj], tab[kTabs + (kC - hj) % kC], tab[kRtLo], tab[kPwLo], d1, dh_help);
+    xch[kAB * hj] = d1;
   }
   // row writes: 16-byte pieces, consecutive threads on consecutive pieces (M / 2 = 6000 per half)
   double2* drow2 = reinterpret_cast<double2*>(drow);
@@ -760,10 +774,11 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
 #endif
   for (int q = t; q < kM / 2; q += kThreads) drow2[q] = xch2[q];
   __syncthreads();
-  if (task3) {
+  if (act) {
 #pragma unroll
     for (int j = 0; j < kC; ++j) xch[lo + kAB * j] = dhi[j];
   }
+  if (helper) xch[kAB * hj] = dh_help;
   __syncthreads();
   for (int q = t; q < kM / 2; q += kThreads) drow2[kM / 2 + q] = xch2[q];
 #if FDLP_DCT_PHASES
