@@ -20,7 +20,7 @@ def main():
     if os.environ.get("FDLP_LIB") != VAR:
         if not os.path.exists(VAR):
             from speech_recognition_tools_amd import _build
-            _build.build(out=VAR, defines=["-DFDLP_DCT_PHASES=1"])
+            _build.build(out=VAR, defines=["-DFDLP_DCT_PHASES=2"])
         env = dict(os.environ, FDLP_LIB=VAR)
         sys.exit(subprocess.call([sys.executable, os.path.abspath(__file__)], env=env))
     import numpy as np
@@ -40,8 +40,9 @@ def main():
     for _ in range(2):
         plan.compute(pcm, [T] * n, rng.randbits2(n * (F - 1)), out=out)
     torch.cuda.synchronize()
-    d = plan.debug_fetch(F * n, keys=("dct",))["dct"][:, :7]
-    ts = d.astype(np.int64)
+    dd = plan.debug_fetch(F * n, keys=("dct",))["dct"]
+    ts = dd[:, :7].astype(np.int64)
+    tg = dd[:, 7:10].astype(np.int64)
     dur = np.diff(ts, axis=1) * 10.0  # ns
     names = ["descriptor+gather+tables+radix20", "twiddle1+exchange1", "radix24+twiddle2", "exchange2+radix25",
              "unpack+post-twiddle", "D rows out"]
@@ -50,6 +51,11 @@ def main():
            "frame_us_mean": float((ts[:, 6] - ts[:, 0]).mean()) / 100.0,
            "phase_us_mean": {k: round(float(v) / 1000.0, 3) for k, v in zip(names, dur.mean(axis=0))},
            "frames_in_flight_mean": float((ts[:, 6] - ts[:, 0]).sum()) / float(t1 - t0)}
+    if tg[:, 0].min() > 0:  # the gather / tables / radix-20 split of the first phase (thread 0's view)
+        g = np.stack([tg[:, 0] - ts[:, 0], tg[:, 1] - tg[:, 0], tg[:, 2] - tg[:, 1], ts[:, 1] - tg[:, 2]], axis=1)
+        res["phase0_split_us_mean"] = {k: round(float(v) / 100.0, 3) for k, v in
+                                       zip(["descriptor+gather", "tables", "radix20+twiddle", "barrier wait"],
+                                           g.mean(axis=0))}
     print(json.dumps(res))
 
 

@@ -565,8 +565,11 @@ __device__ __forceinline__ void pass3_task(int t, int& k1, int& k2a, int& mode) 
 }
 }  // namespace dct1
 
+#ifndef FDLP_DCT_PREFETCH
+#define FDLP_DCT_PREFETCH 0  // 1: L2 prefetch of the PCM of the frame 256 workgroups ahead (A/B builds)
+#endif
 #ifndef FDLP_DCT_PHASES
-#define FDLP_DCT_PHASES 0  // 1: timing build only - thread 0 overwrites D[f][0..7] with phase timestamps
+#define FDLP_DCT_PHASES 0  // 1 / 2: timing builds only - thread 0 overwrites D[f][0..9] with phase timestamps
 #endif
 __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, const void* __restrict__ pcm,
                                                                    int pcm_kind, const int16_t* __restrict__ noise,
@@ -581,6 +584,7 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
   constexpr int N = 2 * kM;
 #if FDLP_DCT_PHASES
   long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tg[4] = {0, 0, 0, 0};  // FDLP_DCT_PHASES == 2: gather / tables / radix-20 split of phase 0
   if (t == 0) ts[0] = wall_clock64();
 #endif
 
@@ -631,8 +635,40 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
     }
   }
   // the tables after the sample gather: their loads overlap the gather's instead of preceding them
+#if FDLP_DCT_PHASES == 2
+  if (t == 0) {
+    // thread 0's gathered samples are in registers: wait for them (timing build only)
+    for (int q1 = 0; q1 < kA; ++q1) asm volatile("" ::"v"(y1[q1].x), "v"(y1[q1].y));
+    tg[0] = wall_clock64();
+  }
+#endif
   for (int q = t; q < kTabs; q += kThreads) tab[q] = c.dct1_tw[q];
+#if FDLP_DCT_PREFETCH
+  // L2 prefetch of the frame kPf ahead (a multiple of 8 workgroups: the same XCD, which runs it about one
+  // round of workgroups later): one int16 load per 80 bytes touches every line of its 48 KB of PCM.
+  // Issued after this frame's gather and table loads, so no wait of this workgroup includes it (the
+  // exchanges and passes below issue no vector loads); its value is kept alive to the kernel's end.
+  int pf_keep = 0;
+  {
+    constexpr int kPf = 256;
+    const int fp = f + kPf;
+    if (fp < (int)gridDim.x && !dense_rows && pcm_kind == 0 && 40 * t < N) {
+      const FrameDesc fdp = frames[fp];
+      const int64_t s0 = (int64_t)fdp.k * c.hop - c.ext;
+      if (s0 >= 0 && s0 + N <= fdp.T) pf_keep = ((const int16_t*)pcm)[fdp.pcm_off + s0 + 40 * t];
+    }
+  }
+#endif
+#if FDLP_DCT_PHASES == 2
+  if (t == 0) tg[1] = wall_clock64();
+#endif
   if (t < kBC) rdft<kA>(y1);
+#if FDLP_DCT_PHASES == 2
+  if (t == 0) {
+    for (int q1 = 0; q1 < kA; ++q1) asm volatile("" ::"v"(y1[q1].x), "v"(y1[q1].y));
+    tg[2] = wall_clock64();
+  }
+#endif
   __syncthreads();  // tables
 #if FDLP_DCT_PHASES
   if (threadIdx.x == 0) ts[1] = wall_clock64();
@@ -781,11 +817,15 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
   if (helper) xch[kAB * hj] = dh_help;
   __syncthreads();
   for (int q = t; q < kM / 2; q += kThreads) drow2[kM / 2 + q] = xch2[q];
+#if FDLP_DCT_PREFETCH
+  asm volatile("" ::"v"(pf_keep));
+#endif
 #if FDLP_DCT_PHASES
   __syncthreads();
   if (t == 0) {
     ts[6] = wall_clock64();
     for (int i = 0; i < 7; ++i) drow[i] = (double)ts[i];
+    for (int i = 0; i < 3; ++i) drow[7 + i] = (double)tg[i];
   }
 #endif
 }
