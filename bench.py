@@ -224,7 +224,7 @@ STAGE_KERNELS = {"dct": ("fdlp::dct_frame", "fdlp::frames_dft1", "fdlp::dft2_dct
                  "autocorr": {"structured": ("fdlp::ac_vsweep_kernel", "fdlp::ac_wrap_kernel", "fdlp::ac_band_kernel"),
                               "structured_mfma": ("fdlp::ac_sweep_kernel", "fdlp::ac_band_kernel"),
                               "direct": ("fdlp::autocorr_kernel",)},
-                 "lpc_env": ("fdlp::durbin8_kernel", "fdlp::lpc_env_lattice_kernel", "fdlp::cep_kernel",
+                 "lpc_env": ("fdlp::durbin4_kernel", "fdlp::durbin8_kernel", "fdlp::lpc_env_lattice_kernel", "fdlp::cep_kernel",
                              "fdlp::env_gemm_kernel"),
                  "ola_log": ("fdlp::ola_log",)}
 
@@ -275,7 +275,7 @@ STAGE_DESC = {"dct": "DCT stage: dct_frame_kernel (one workgroup per frame, Makh
                                          "by the VALU and matrix pipes",
                            "structured_mfma": "autocorr stage: ac_sweep_kernel + ac_band_kernel (v_mfma_f64_16x16x4f64)",
                            "direct": "autocorr stage: autocorr_kernel (v_mfma_f64_16x16x4f64)"},
-              "lpc_env": "LPC stage: durbin8_kernel (Levinson-Durbin) + cepstrum + envelope kernels (fp64)",
+              "lpc_env": "LPC stage: durbin4_kernel (Levinson-Durbin) + cepstrum + envelope kernels (fp64)",
               "ola_log": "OLA + log stage: ola_log_tiled_kernel"}
 
 
@@ -405,6 +405,8 @@ def parse_args(argv=None):
     ap.add_argument("--pipeline", type=int, default=None, help="sub-batches over two streams (plan default 1)")
     ap.add_argument("--dct-path", default="auto", choices=["auto", "four_step"],
                     help="DCT stage: auto (one dct_frame_kernel per frame at N = 24000) or the four-step pair")
+    ap.add_argument("--lpc-path", default="auto", choices=["auto", "lattice8", "lds"],
+                    help="Durbin kernel (A/B): auto = durbin4_kernel for the recipes' p = 150")
     ap.add_argument("--inflight", type=int, default=4,
                     help="device batches in flight per GPU: independent plans on their own HIP streams, each "
                          "featurising its own batch every step (their kernels overlap on the device)")
@@ -526,6 +528,7 @@ def main():
     plans = [plan] + [FdlpPlan(cfg, device=dev.index, max_frames=frames) for _ in range(B - 1)]
     for pl in plans:
         pl.set_dct_path(args.dct_path)
+        pl.set_lpc_path(args.lpc_path)
     shifts = [7919 * b for b in range(B)]
     pcms = [pcm] + [torch.roll(pcm, shifts[b]) for b in range(1, B)]
     outs = [out] + [torch.empty_like(out) for _ in range(B - 1)]

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define FDLP_ABI_VERSION 5
+#define FDLP_ABI_VERSION 6
 
 enum {
   FDLP_OK = 0,
@@ -161,12 +161,15 @@ int fdlp_set_debug(fdlp_plan* plan, int32_t keep_intermediates);
 int fdlp_set_autocorr_path(fdlp_plan* plan, int32_t path);
 int fdlp_autocorr_path(const fdlp_plan* plan);
 /* LPC stage (Levinson-Durbin + cepstrum + envelope).  FDLP_LPC_AUTO (plan default): the register-resident
- * lattice kernels (durbin8_kernel for 128 <= p <= 183, then the cepstrum / envelope kernel); FDLP_LPC_LDS:
+ * lattice kernels (durbin4_kernel, 4 lanes per item, for 128 <= p <= 150; durbin8_kernel, 8 lanes per item,
+ * for 150 < p <= 183; then the cepstrum / envelope kernel); FDLP_LPC_LATTICE8 (ABI 6): the same with
+ * durbin8_kernel for every 128 <= p <= 183 (cross-check of durbin4_kernel); FDLP_LPC_LDS:
  * the LDS Durbin kernel for every p (the fallback for p > 255 and an independent cross-check; its
  * order-k dot products are summed in another order).  The only switches between kernel variants are
  * these explicit calls: nothing is read from the environment (ABI 4). */
 #define FDLP_LPC_AUTO 0
 #define FDLP_LPC_LDS 1
+#define FDLP_LPC_LATTICE8 2
 int fdlp_set_lpc_path(fdlp_plan* plan, int32_t path);
 /* DCT stage (ABI 5).  FDLP_DCT_AUTO (plan default): for the recipes' frame length N = 24000 one kernel per
  * frame (dct_frame_kernel: the packed 12000-point FFT as three in-register passes with LDS exchanges,
@@ -195,7 +198,9 @@ int fdlp_set_pipeline(fdlp_plan* plan, int32_t n_sub);
  * cep [F,B,coeff_num]; env [F,B,kk]. */
 int fdlp_debug_fetch(fdlp_plan* plan, int32_t n_frames, double* dct, double* r, double* a,
                      double* gg, double* cep, double* env);
-/* Same for the frames [first_frame, first_frame + n_frames) of the most recent batch (ABI 3). */
+/* Same for the frames [first_frame, first_frame + n_frames) of the most recent batch (ABI 3).
+ * a and cep need fdlp_set_debug(plan, 1) before that compute (their workspaces are allocated by it;
+ * FDLP_E_INVALID otherwise); dct, r, gg and env are always available. */
 int fdlp_debug_fetch_range(fdlp_plan* plan, int32_t first_frame, int32_t n_frames, double* dct, double* r,
                            double* a, double* gg, double* cep, double* env);
 

@@ -7,7 +7,9 @@
 # HIP -- HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES if set, else the KFD
 # topology's GPU nodes -- so a recipe that calls the driver unchanged, e.g. --cmd "$train_cmd" --nj 20
 # (e2e/wsj/run_fdlp_e1.sh:196), spreads its JOBs over the node), --jobs_per_gpu K (without $cmd: at most
-# N*K JOBs run at once; default 2).
+# N*K JOBs run at once; default 2), --job_mem / --job_gpu (the resource request a $cmd launcher gets for
+# every JOB: "$cmd --mem 5G --gpu 1 JOB=1:$nj ...", the reference's --mem 5G (:92, :141) plus one GPU, so
+# queue.pl / slurm.pl allocate the MI355X the JOB runs on; run.pl ignores both; --job_gpu 0 drops it).
 #
 #   make_FDLPspectrum_feats.sh [--opts] <data_dir> <feat_dir>
 # Inputs: <data_dir>/wav.scp or <data_dir>/segments.  Outputs: <data_dir>/feats.scp,
@@ -40,6 +42,8 @@ jobs_per_gpu=2  # two JOBs per GPU overlap each other's latency-bound kernels (D
 compute_cmvn=false   # also write <data_dir>/cmvn.ark (global CMVN stats, fused on the device)
 seed=
 noise_seed=
+job_mem=5G     # $cmd --mem (the reference driver's request, make_FDLPspectrum_feats.sh:92, :141)
+job_gpu=1      # $cmd --gpu (0: no GPU request)
 
 if [ -f utils/parse_options.sh ]; then
   . utils/parse_options.sh || exit 1
@@ -108,7 +112,10 @@ run_jobs() {  # run_jobs <list-pattern containing JOB> <scp-type-opt>
   local cmvn_opt=
   $compute_cmvn && cmvn_opt="--cmvn_stats $feat_dir/cmvn_${name}.JOB.mat"
   if [ -n "$cmd" ]; then
-    $cmd JOB=1:$nj "$log_dir/feats_${name}.JOB.log" \
+    local req=
+    [ -n "$job_mem" ] && req="--mem $job_mem"
+    [ "${job_gpu:-0}" != 0 ] && req="$req --gpu $job_gpu"
+    $cmd $req JOB=1:$nj "$log_dir/feats_${name}.JOB.log" \
       python3 "$cli" "$pattern" "$feat_dir/melspec_${name}.JOB" $add_opts $cmvn_opt $stype --device_rr=JOB,$ngpu \
         --fbank_type=$fbank_type --gamma_weight=$gamma_weight --add_reverb=$add_reverb \
         --add_noise=$add_noise --coeff_num=$coeff_num --coeff_range=$coeff_range --order=$order \

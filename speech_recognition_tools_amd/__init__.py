@@ -4,8 +4,10 @@ sadhusamik/speech_recognition_tools: src/featgen/computeFDLPSpectrogram.py + fea
 The compute path is libfdlp_hip.so (hand-written gfx950 HIP kernels behind include/fdlp.h); loading it
 fails loudly when the library is missing (there is no fallback).  The names below load lazily, so the
 native JOB runner of compute-fdlp-feats can choose the HIP runtime before the library is loaded
-(speech_recognition_tools_amd._hip_runtime); a process that has imported torch gets
-torch.ops.fdlp.spectrogram registered on import.
+(speech_recognition_tools_amd._hip_runtime).  torch.ops.fdlp.spectrogram is registered by importing
+speech_recognition_tools_amd.ops: on package import when torch was imported first, otherwise when FdlpPlan
+is first touched -- a process that imports torch after this package and wants the op before it creates a
+plan imports speech_recognition_tools_amd.ops itself.
 """
 import importlib
 import sys

@@ -31,28 +31,35 @@ def stale():
 
 
 def build(force=False, verbose=False, out=None, defines=()):
-    """out / defines: an A/B variant of the library (e.g. -DFDLP_D8_CHAINS=2) at another path, loaded
+    """out / defines: an A/B variant of the library (e.g. -DFDLP_DEVICE_CHECKS=1) at another path, loaded
     through FDLP_LIB; the default build is LIB."""
     target = out or LIB
     if not force and out is None and not stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     os.makedirs(os.path.dirname(os.path.abspath(target)), exist_ok=True)
-    objs, procs = [], []
+    objs, cmds = [], []
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function",
              "-munsafe-fp-atomics"] + list(defines)
-    for src in SOURCES:  # the translation units compile in parallel
-        obj = os.path.join(LIBDIR, src + ".ab.o" if out else src + ".o")
+    tag = "." + os.path.basename(target).replace(".", "_") if out else ""
+    for src in SOURCES:
+        obj = os.path.join(LIBDIR, src + tag + ".o")
         lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "c++"]
         cmd = [hipcc()] + flags + lang + ["-c", os.path.join(CSRC, src), "-o", obj]
         if src.endswith(".cpp"):
             cmd = [hipcc(), "-O3", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-Wall",
-                   "-x", "c++", "-c", os.path.join(CSRC, src), "-o", obj]
+                   "-x", "c++", "-c", os.path.join(CSRC, src), "-o", obj] + [d for d in defines if d.startswith("-D")]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        procs.append((subprocess.Popen(cmd), cmd))
+        cmds.append(cmd)
         objs.append(obj)
-    failed = [cmd for p, cmd in procs if p.wait() != 0]
+    # the translation units compile in parallel, at most one per host CPU; every started compiler is
+    # waited for (subprocess.run), and the first failure is raised after all have finished
+    from concurrent.futures import ThreadPoolExecutor
+    workers = max(1, min(len(cmds), os.cpu_count() or 1))
+    with ThreadPoolExecutor(max_workers=workers) as pool:
+        rcs = list(pool.map(lambda c: subprocess.run(c).returncode, cmds))
+    failed = [c for c, rc in zip(cmds, rcs) if rc != 0]
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
     tmp = target + ".tmp"

@@ -183,7 +183,7 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.fdlp_abi_version() != 5:
+    if lib.fdlp_abi_version() != 6:
         raise ImportError("libfdlp_hip.so ABI mismatch")
     return lib
 

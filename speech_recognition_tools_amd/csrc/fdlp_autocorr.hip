@@ -608,32 +608,22 @@ __global__ __launch_bounds__(64) void ac_wrap_kernel(DevConsts c, const double* 
 // -----------------------------------------------------------------------------------------
 
 constexpr int kVsMirror = 16;
-#ifndef FDLP_VS_SKIRT3
-#define FDLP_VS_SKIRT3 0  // 1: skirt sweeps at three waves per SIMD (320-position ring, 128-position chunks, one
-                          // parked row; 137 VGPRs): measured 1.56 -> 2.19 ms (r03s), kept as a compile-time variant
-#endif
 // ring positions per unit (a power of two is not required: slots are taken modulo the ring) and the LDS
-// row stride; rows of 352 / 544 doubles keep each ds_read_b128 lane group on 64 distinct banks for the
-// 10-double lane stride of the window reads
+// row stride; rows of 544 doubles keep each ds_read_b128 lane group on 64 distinct banks for the
+// 10-double lane stride of the window reads.  (Skirt sweeps at three waves per SIMD -- a 320-position
+// ring, 128-position chunks, one parked row -- measured 1.56 -> 2.19 ms, r03s: not kept.)
 template <int C>
-constexpr int vs_ring() { return (C == 0 && FDLP_VS_SKIRT3) ? 320 : 512; }
+constexpr int vs_ring() { return 512; }
 template <int C>
-constexpr int vs_row() { return (C == 0 && FDLP_VS_SKIRT3) ? 352 : 544; }
+constexpr int vs_row() { return 544; }
 // positions staged per chunk; the prefetch of the next chunk has to cover the HBM latency under load
 // (64 positions, ~3000 cycles of FMAs, measured too short).  The flat sweep keeps its chains in
 // registers, so it stages 128 at a time to stay at two waves per SIMD.
 template <int A, int C>
-constexpr int vs_chunk() { return (C == 0 && !FDLP_VS_SKIRT3 && 18 * A < vs_ring<C>() - 256) ? 256 : 128; }
+constexpr int vs_chunk() { return (C == 0 && 18 * A < vs_ring<C>() - 256) ? 256 : 128; }
 template <int C>
-constexpr int vs_waves_per_simd() { return (C == 0 && FDLP_VS_SKIRT3) ? 3 : 2; }
+constexpr int vs_waves_per_simd() { return 2; }
 
-template <int A, int V = 0>
-__device__ __forceinline__ void vs_bcast_all(double (&bb)[A], double cur) {
-  if constexpr (V < A) {
-    bb[V] = row_bcast<V>(cur);
-    vs_bcast_all<A, V + 1>(bb, cur);
-  }
-}
 template <int A, int V = 0>
 __device__ __forceinline__ void vs_fma_rows(double (&acc)[A], double cur, const double (&lo)[A], const double (&hi)[A]) {
   if constexpr (V < A) {
@@ -645,20 +635,12 @@ __device__ __forceinline__ void vs_fma_rows(double (&acc)[A], double cur, const 
 template <int A>
 __device__ __forceinline__ void vs_fma_block(double (&acc)[A], double cur, const double (&lo)[A],
                                              const double (&hi)[A]) {
-#ifdef FDLP_VSWEEP_DPP_MOV
-  double bb[A];
-  vs_bcast_all<A>(bb, cur);
-#pragma unroll
-  for (int v = 0; v < A; ++v)
-#pragma unroll
-    for (int u = 0; u < A; ++u) acc[u] = fma(bb[v], (v + u < A) ? lo[v + u] : hi[v + u - A], acc[u]);
-#else
   // the DPP source must be two wait states past its VALU write (the compiler cannot see the DPP
-  // inside the asm): copy it through one asm that ends in the wait
+  // inside the asm): copy it through one asm that ends in the wait.  (Broadcasting by v_mov_dpp into
+  // registers first and plain FMAs: slower, r03.)
   double cm;
   asm volatile("v_mov_b64 %0, %1\n\ts_nop 1" : "=v"(cm) : "v"(cur));
   vs_fma_rows<A>(acc, cm, lo, hi);
-#endif
 }
 
 template <int A, int C>
@@ -783,7 +765,7 @@ __global__ __launch_bounds__(64, vs_waves_per_simd<C>()) void ac_vsweep_kernel(D
   // right after the ring commit and before the next prefetch.  A VMEM store's data registers must
   // not be rewritten before the store completes (vmcnt, in order with the prefetch loads), so storing
   // from reused registers would put a wait for the prefetch at the head of every block.
-  constexpr int P = (C == 0 && !FDLP_VS_SKIRT3) ? 2 : 1;
+  constexpr int P = C == 0 ? 2 : 1;
   double* const outb = kind == 0 ? rlow : (kind == 1 ? rup : rflat);
   double pend[P][A];
   int64_t prow[P];

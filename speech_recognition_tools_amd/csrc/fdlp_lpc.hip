@@ -572,24 +572,20 @@ __device__ __forceinline__ void contig_durbin(double (&A)[S], double (&B)[S], do
 // envelope phases (DM = 2), which then run at their own occupancy.  Same recursion as contig_step
 // (features.py:226-228); only the summation order of the order-k dot product differs (8 lane partials).
 // -----------------------------------------------------------------------------------------
-#ifndef FDLP_D8_CHAINS
-#define FDLP_D8_CHAINS 4  // 2 or 4
-#endif
-#ifndef FDLP_D8_NEWTON
-#define FDLP_D8_NEWTON 2  // Newton steps after v_rcp_f64 for 1/E
-#endif
+constexpr int kD8Chains = 4;  // the next order's dot product in 4 chains (2: no difference, 1.13 vs 1.14 ms)
+constexpr int kNewton = 2;    // Newton steps after v_rcp_f64 for 1/E (one: parity green, time within noise)
 template <int S>
 __device__ __forceinline__ void c8_step(double (&A)[S], const double (&Bs)[S], double (&Bd)[S],
                                         const double (&R1)[S], double& part, double& E, bool first) {
   const double acc = sum8(part);  // r_k + sum_i a_i r_{k-i}
   double rE = __builtin_amdgcn_rcp(E);
 #pragma unroll
-  for (int it = 0; it < FDLP_D8_NEWTON; ++it) rE = fma(rE, fma(-E, rE, 1.0), rE);
+  for (int it = 0; it < kNewton; ++it) rE = fma(rE, fma(-E, rE, 1.0), rE);
   const double kappa = -acc * rE;
   const double zs = __builtin_amdgcn_update_dpp(0.0, Bs[S - 1], 0x111, 0xF, 0xF, true);  // row_shr:1
   const double z0 = first ? 0.0 : zs;
   // the next order's dot product in D independent chains (the chain, not the issue, bounds small S)
-  constexpr int D = FDLP_D8_CHAINS;
+  constexpr int D = kD8Chains;
   double pc[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) pc[d] = 0.0;
@@ -727,6 +723,178 @@ __global__ __launch_bounds__(64, 2) void durbin8_kernel(const double* __restrict
   double E = r0;
   c8_durbin<SL8, 1>(A1, B1, R11, part, E, rl, sc, p, li, valid, r0, a + (int64_t)(valid ? item : 0) * astride,
                     gg + (valid ? item : 0), astride);
+}
+
+// -----------------------------------------------------------------------------------------
+// The same lattice Durbin with 4 lanes per item (a DPP quad is an item, 16 items per wave; the recipes'
+// p = 150 and every p <= 4 SL4 - 2).  Per order a wave issues 3 S FMAs (A, B, the next order's dot
+// product) and ~17 instructions of cross-lane work (the quad sum, kappa, the B shift, E and 1/E), so
+// the cross-lane part is paid once per 16 items instead of 8: ~36 % fewer VALU instructions per item
+// than durbin8_kernel at p = 150.  What makes it fit:
+// * B is updated in place (slots in descending order: B[j-1] is still the previous order's when B[j]
+//   and A[j] read it), so an order needs A, B and R1 only: 3 x 38 doubles at the last phase.
+// * A phase S (S positions per lane, capacity 4 S) runs orders k <= 4 S - 2, so the last position
+//   4 S - 1 of B is exactly 0 (b_m = a_{k-m}, m > k): the row_shr:1 of B's last slot then hands the next
+//   item's first lane a 0 by itself (the quad boundaries are not row boundaries), no select.
+// * 1/E for the next order (rcp + two Newton steps) is computed right after kappa, beside the order's
+//   FMAs, so the serial part of an order is only the dot-product tail, the quad sum and kappa.
+// * No r staging: R1 is re-laid out with A through the item's LDS image (R1 first, while B is already
+//   dead), the 8 positions a phase adds come from global loads issued one phase ahead.  16 items x 156
+//   doubles = 19.6 KB of LDS per wave, two waves per SIMD.
+// Phases S = 1, 3, 5, ... (odd: the lane strides S and S + 2 with the item stride 156 = -4 mod 32 doubles
+// put the 32 lanes of a ds_read_b64 group and the 16 of a ds_write_b64 group on distinct banks), then SL4.
+// Same recursion and the same kappa / E / 1/E arithmetic as c8_step (features.py:226-228); the order-k dot
+// product is summed over 4 lane partials of 2 chains instead of 8 lanes of 4 chains.
+// -----------------------------------------------------------------------------------------
+__device__ __forceinline__ double sum4(double v) {  // over a DPP quad; every lane gets the same (bitwise) value
+  v += dpp_f64<0xB1>(v);  // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);  // quad_perm [2,3,0,1]
+  return v;
+}
+__device__ __forceinline__ double rcp_newton(double E) {
+  double rE = __builtin_amdgcn_rcp(E);
+#pragma unroll
+  for (int it = 0; it < kNewton; ++it) rE = fma(rE, fma(-E, rE, 1.0), rE);
+  return rE;
+}
+
+template <int S>
+__device__ __forceinline__ void c4_step(double (&A)[S], double (&B)[S], const double (&R1)[S], double& part,
+                                        double& E, double& rE) {
+  const double acc = sum4(part);  // r_k + sum_i a_i r_{k-i}
+  const double kappa = -acc * rE;
+  // z B at slot 0: lane li - 1's last slot (row_shr:1; row edges take 0 from bound_ctrl, the other
+  // quad edges the exact 0 of position 4 S - 1)
+  const double z0 = __builtin_amdgcn_update_dpp(0.0, B[S - 1], 0x111, 0xF, 0xF, true);
+  constexpr int D = S >= 4 ? 2 : 1;  // dot-product chains
+  double pc[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) pc[d] = 0.0;
+#pragma unroll
+  for (int j = S - 1; j >= 0; --j) {
+    const double zb = j == 0 ? z0 : B[j - 1];
+    const double bn = fma(kappa, A[j], zb);
+    A[j] = fma(kappa, zb, A[j]);
+    B[j] = bn;
+    pc[j % D] = fma(bn, R1[j], pc[j % D]);
+  }
+  if constexpr (D == 2) part = pc[0] + pc[1];
+  else part = pc[0];
+  E = E * (1.0 - kappa * kappa);
+  rE = rcp_newton(E);
+}
+
+// LDS doubles per item: the image of 4 S positions plus the 8 a phase adds, = 28 mod 32 (see above)
+__host__ __device__ constexpr int c4_item_stride(int SL4) {
+  const int need = 4 * (SL4 - 1) + 8 > 4 * SL4 ? 4 * (SL4 - 1) + 8 : 4 * SL4;
+  return need + ((28 - need % 32) + 32) % 32;
+}
+constexpr int kC4Guard = 16;  // doubles below item 0's image (the mirrored B reads reach index -9)
+
+// Orders [k0, min(p, 4 S - 2)] of phase S, then the next phase.  Returns (in cap) 4 S of the phase that
+// ends at order p and leaves its A in img (positions < cap; exactly 0 past p), gg in g.
+template <int SL4, int S>
+__device__ __forceinline__ void c4_durbin(double (&A)[S], double (&B)[S], double (&R1)[S], double& part, double& E,
+                                          double& rE, double* img, const double* rrow, int p, int li, bool valid,
+                                          double r0, int k0, int& cap, double& g) {
+  const int k1 = min(p, 4 * S - 2);
+  constexpr int SN = S + 2 <= SL4 ? S + 2 : SL4;
+  double rn[2] = {0.0, 0.0};  // R1 of the 8 positions the next phase adds: 4 S + 2 li + t
+  if constexpr (SN > S) {
+    if (k1 < p) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int m = 4 * S + 2 * li + t;
+        if (valid && m <= p) rn[t] = rrow[m + 1];
+      }
+    }
+  }
+  for (int k = k0; k <= k1; ++k) c4_step<S>(A, B, R1, part, E, rE);
+  if constexpr (SN > S) {
+    if (k1 < p) {
+      // R1 first (B is dead: it is read back mirrored from A's image), then A
+      double R1n[SN], An[SN], Bn[SN];
+      wave_lds_sync();
+#pragma unroll
+      for (int j = 0; j < S; ++j) img[li * S + j] = R1[j];
+      img[4 * S + 2 * li] = rn[0];
+      img[4 * S + 2 * li + 1] = rn[1];
+      wave_lds_sync();
+#pragma unroll
+      for (int j = 0; j < SN; ++j) R1n[j] = img[li * SN + j];
+      wave_lds_sync();
+#pragma unroll
+      for (int j = 0; j < S; ++j) img[li * S + j] = A[j];
+      wave_lds_sync();
+      // A past k1 is exactly 0; b_m = a_{k1-m} (0 for m > k1: reads down to index -9 land in the guard
+      // or the previous item's image and are dropped by the select)
+#pragma unroll
+      for (int j = 0; j < SN; ++j) {
+        const int m = li * SN + j;
+        const double v = img[m];
+        An[j] = m <= k1 ? v : 0.0;
+      }
+#pragma unroll
+      for (int j = 0; j < SN; ++j) {
+        const int m = k1 - li * SN - j;
+        const double v = img[m];
+        Bn[j] = m >= 0 ? v : 0.0;
+      }
+      c4_durbin<SL4, SN>(An, Bn, R1n, part, E, rE, img, rrow, p, li, valid, r0, k1 + 1, cap, g);
+      return;
+    }
+  }
+  // order p done: gg = r0 + sum_{m=0}^{p} a_m r_{m+1} (the reference's off-by-one, features.py:228)
+  double q0 = 0.0, q1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    if (j & 1) q1 = fma(A[j], R1[j], q1);
+    else q0 = fma(A[j], R1[j], q0);
+  }
+  g = r0 + sum4(q0 + q1);
+  wave_lds_sync();
+#pragma unroll
+  for (int j = 0; j < S; ++j) img[li * S + j] = A[j];
+  cap = 4 * S;
+}
+
+// one wave per 16 items, p <= 4 SL4 - 2 <= astride; a / gg: [items, astride] (zero past p) / [items].
+// The rows leave through the LDS images as coalesced 16-byte stores.
+template <int SL4>
+__global__ __launch_bounds__(64, 2) void durbin4_kernel(const double* __restrict__ r, int nlags, int p, int items,
+                                                        double* __restrict__ a, double* __restrict__ gg, int astride) {
+  constexpr int kItem = c4_item_stride(SL4);
+  __shared__ double lds[kC4Guard + 16 * kItem];
+  const int lane = threadIdx.x;
+  const int li = lane & 3;
+  const int ii = lane >> 2;
+  const int item0 = blockIdx.x * 16;
+  const int item = item0 + ii;
+  const bool valid = item < items;
+  const double* rrow = r + (int64_t)(valid ? item : 0) * nlags;
+  double* img = lds + kC4Guard + ii * kItem;
+  const double r0 = valid ? rrow[0] : 1.0;
+  double A[1] = {li == 0 ? 1.0 : 0.0}, B[1] = {li == 0 ? 1.0 : 0.0};
+  double R1[1] = {valid && li <= p ? rrow[li + 1] : 0.0};
+  double part = li == 0 ? R1[0] : 0.0;  // order 1: b^(0) . R1 = r_1
+  double E = r0, rE = rcp_newton(r0);
+  int cap = 0;
+  double g = 0.0;
+  c4_durbin<SL4, 1>(A, B, R1, part, E, rE, img, rrow, p, li, valid, r0, 1, cap, g);
+  if (valid && li == 0) gg[item] = g;
+  wave_lds_sync();
+  const int half = astride >> 1;
+  for (int i = 0; i < 16; ++i) {
+    if (item0 + i >= items) break;
+    const double* src = lds + kC4Guard + i * kItem;
+    double2* dst = reinterpret_cast<double2*>(a + (int64_t)(item0 + i) * astride);
+    for (int h = lane; h < half; h += 64) {
+      const int m = 2 * h;
+      double2 v = make_double2(0.0, 0.0);
+      if (m < cap) v = *reinterpret_cast<const double2*>(src + m);  // cap is even: both or neither
+      dst[h] = v;
+    }
+  }
 }
 
 // lpc_env with the lattice Durbin: persistent waves (grid-stride over groups of 4 items), r read
@@ -1147,15 +1315,12 @@ int lpc_env_region(int p, int M) {
 
 // Lattice-kernel instantiation of a plan: calls fn(integral_constant<SL>, integral_constant<CB>) or
 // returns hipErrorNotSupported when the plan runs the LDS Durbin (lpc_env_kernel).
-#ifndef FDLP_CEP_SB_ALWAYS
-#define FDLP_CEP_SB_ALWAYS 0  // 1: the super-block cepstrum (CB < 0) also for M <= 112 (A/B builds)
-#endif
 template <class Fn>
 static hipError_t lattice_dispatch_sl(const DevConsts& c, Fn&& fn) {
   using std::integral_constant;
   const int SL = (c.p + 1 + 15) / 16;
   if (SL > 16 || c.lpc_mode == 1) return hipErrorNotSupported;
-  if (!FDLP_CEP_SB_ALWAYS && c.M <= 16 * 7 && SL >= 9 && SL <= 11) {  // register-broadcast cepstrum (recipes: p 150, M 100)
+  if (c.M <= 16 * 7 && SL >= 9 && SL <= 11) {  // register-broadcast cepstrum (recipes: p 150, M 100)
     switch (SL) {
       case 9: return fn(integral_constant<int, 9>{}, integral_constant<int, 7>{});
       case 10: return fn(integral_constant<int, 10>{}, integral_constant<int, 7>{});
@@ -1163,7 +1328,7 @@ static hipError_t lattice_dispatch_sl(const DevConsts& c, Fn&& fn) {
       default: break;
     }
   }
-  if ((FDLP_CEP_SB_ALWAYS || c.M > 16 * 7) && SL >= 9 && SL <= 11) {  // the same over a sliding window (REVERB: M 450)
+  if (c.M > 16 * 7 && SL >= 9 && SL <= 11) {  // the same over a sliding window (REVERB: M 450)
     switch (SL) {
       case 9: return fn(integral_constant<int, 9>{}, integral_constant<int, -1>{});
       case 10: return fn(integral_constant<int, 10>{}, integral_constant<int, -1>{});
@@ -1199,6 +1364,12 @@ static hipError_t durbin8_dispatch(int p, Fn&& fn) {
   }
 }
 
+// durbin4_kernel (4 lanes per item): one instantiation, SL4 = 38, for 128 <= p <= 150 (the recipes' 150)
+constexpr int kDurbin4SL = 38;
+static bool durbin4_fits(const DevConsts& c) {
+  return c.lpc_mode == 0 && c.p >= 128 && c.p <= 4 * kDurbin4SL - 2;
+}
+
 // fn(integral_constant<SL>, integral_constant<CB>, integral_constant<int, DM>)
 template <class Fn>
 static hipError_t lattice_dispatch(const DevConsts& c, Fn&& fn) {
@@ -1228,7 +1399,8 @@ static size_t lattice_lds(const DevConsts& c, int CB, int SL) {
 hipError_t prepare_lpc_env(DevConsts& c) {
   // c.lpc_mode (fdlp_set_lpc_path): 0 = the lattice kernels (durbin8_kernel where p fits it, then the
   // register cepstrum / envelope kernel), 1 = the LDS Durbin kernel (lpc_env_kernel) for every p
-  c.lpc_split = c.lpc_mode == 0 && durbin8_fits(c.p);
+  // 2 = the lattice kernels with durbin8_kernel also where durbin4_kernel fits (cross-check)
+  c.lpc_split = (c.lpc_mode == 0 || c.lpc_mode == 2) && durbin8_fits(c.p);
   c.lpc_astride = 0;
   c.lpc_blocks = 0;
   int dev = 0, cus = 0;
@@ -1241,7 +1413,8 @@ hipError_t prepare_lpc_env(DevConsts& c) {
     constexpr int CT = decltype(ct)::value;
     const size_t lds = lattice_lds(c, CB, SL);
     if (CT == kDmExt)  // >= the durbin8 image (8 SL8 positions written per row) and the cepstrum's a area
-      c.lpc_astride = (std::max(CB != 0 ? lattice_la_len(c, CB, SL) : c.p + 1, 8 * durbin8_sl8(c.p)) + 15) / 16 * 16;
+      c.lpc_astride = (std::max({CB != 0 ? lattice_la_len(c, CB, SL) : c.p + 1, 8 * durbin8_sl8(c.p),
+                                 durbin4_fits(c) ? 4 * kDurbin4SL : 0}) + 15) / 16 * 16;
     if (lds > 65536) {
       const hipError_t a = hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL, CB, CT>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1266,7 +1439,12 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
   if (c.lpc_blocks > 0 && c.lpc_split) {  // the Durbin first, into a_ws / gg_ws
     if (!a_ws || !gg_ws) return hipErrorInvalidValue;
     double* gd = gg_out ? gg_out : gg_ws;
-    const hipError_t e = durbin8_dispatch(c.p, [&](auto sl8) -> hipError_t {
+    const hipError_t e = durbin4_fits(c) ? [&]() -> hipError_t {
+      if (c.lpc_astride < 4 * kDurbin4SL) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((durbin4_kernel<kDurbin4SL>), dim3((items + 15) / 16), dim3(64), 0, s, r, c.nlags, c.p, items,
+                         a_ws, gd, c.lpc_astride);
+      return hipGetLastError();
+    }() : durbin8_dispatch(c.p, [&](auto sl8) -> hipError_t {
       constexpr int SL8 = decltype(sl8)::value;
       hipLaunchKernelGGL((durbin8_kernel<SL8>), dim3((items + 7) / 8), dim3(64), 0, s, r, c.nlags, c.p, items, a_ws, gd,
                          c.lpc_astride);

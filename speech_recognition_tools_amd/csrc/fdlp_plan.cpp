@@ -1091,12 +1091,12 @@ int fdlp_plan_regions(const fdlp_plan* p, int32_t* m1, int32_t* m2) {
 }
 
 int fdlp_set_lpc_path(fdlp_plan* p, int32_t path) {
-  if (!p || (path != FDLP_LPC_AUTO && path != FDLP_LPC_LDS))
-    return fail(FDLP_E_INVALID, "fdlp_set_lpc_path: need a plan and FDLP_LPC_AUTO or FDLP_LPC_LDS");
+  if (!p || (path != FDLP_LPC_AUTO && path != FDLP_LPC_LDS && path != FDLP_LPC_LATTICE8))
+    return fail(FDLP_E_INVALID, "fdlp_set_lpc_path: need a plan and FDLP_LPC_AUTO, FDLP_LPC_LDS or FDLP_LPC_LATTICE8");
   if (p->device < 0) return fail(FDLP_E_INVALID, "fdlp_set_lpc_path: host-only plan");
   DeviceGuard dg(p->device);
   if (dg.status() != hipSuccess) return fail(FDLP_E_HIP, "hipSetDevice failed");
-  p->dc.lpc_mode = path == FDLP_LPC_LDS ? 1 : 0;
+  p->dc.lpc_mode = path;
   if (fdlp::prepare_lpc_env(p->dc) != hipSuccess) return fail(FDLP_E_HIP, "LPC kernel launch setup failed");
   if (p->dc.lpc_split && !p->ws.a_pad &&
       hipMalloc((void**)&p->ws.a_pad, sizeof(double) * (size_t)p->max_frames * p->B * p->dc.lpc_astride) != hipSuccess)
@@ -1135,16 +1135,17 @@ int fdlp_autocorr_path(const fdlp_plan* p) {
 
 int fdlp_set_debug(fdlp_plan* p, int32_t keep_intermediates) {
   if (!p) return fail(FDLP_E_INVALID, "fdlp_set_debug: null plan");
-  p->debug_intermediates = keep_intermediates != 0;
   // a [items, p+1] and cep [items, M] exist only for debugging (and cep for the modspec output): allocated
-  // here, not at plan creation (for REVERB's M = 450 the two are ~0.8 GB at 2048 frames)
-  if (p->debug_intermediates && p->device >= 0) {
+  // here, not at plan creation (for REVERB's M = 450 the two are ~0.8 GB at 2048 frames).  The flag is set
+  // only once both exist: fdlp_compute offsets them per sub-batch when it is set.
+  if (keep_intermediates != 0 && p->device >= 0) {
     DeviceGuard dg(p->device);
     HIP_TRY(dg.status());
     const size_t items = (size_t)p->max_frames * p->B;
     if (!p->ws.a) HIP_TRY(hipMalloc((void**)&p->ws.a, sizeof(double) * items * (p->p + 1)));
     if (!p->ws.cep) HIP_TRY(hipMalloc((void**)&p->ws.cep, sizeof(double) * items * p->M));
   }
+  p->debug_intermediates = keep_intermediates != 0;
   return FDLP_OK;
 }
 

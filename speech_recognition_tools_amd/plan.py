@@ -168,11 +168,13 @@ class FdlpPlan:
     def set_autocorr_path(self, path: str = "auto"):
         check(lib.fdlp_set_autocorr_path(self._h, self.AUTOCORR_PATHS[path]))
 
-    LPC_PATHS = {"auto": 0, "lds": 1}
+    LPC_PATHS = {"auto": 0, "lds": 1, "lattice8": 2}
 
     def set_lpc_path(self, path: str = "auto"):
-        """'auto': the lattice kernels (durbin8_kernel + register cepstrum / envelope); 'lds': the LDS
-        Durbin kernel (the large-p fallback, an independent cross-check)."""
+        """'auto': the lattice kernels (durbin4_kernel for 128 <= p <= 150, durbin8_kernel above, then the
+        register cepstrum / envelope kernel); 'lattice8': the same with durbin8_kernel for every p it
+        covers (cross-check of durbin4_kernel); 'lds': the LDS Durbin kernel (the large-p fallback, an
+        independent cross-check)."""
         check(lib.fdlp_set_lpc_path(self._h, self.LPC_PATHS[path]))
 
     DCT_PATHS = {"auto": 0, "four_step": 1}

@@ -71,6 +71,28 @@ def test_driver_cmd_branch_spreads_jobs_over_gpus(tmp_path, monkeypatch, nj, ngp
         assert "--device_rr=%d,%d" % (n, ngpu) in argv
         devices.append(_resolve(argv))
     assert devices == [(n - 1) % ngpu for n in range(1, nj + 1)]
+    # the resource request the launcher gets for the JOB array: the reference's --mem 5G
+    # (recipes/timit/local_pyspeech/make_FDLPspectrum_feats.sh:92) plus one GPU per JOB
+    assert (tmp_path / "cmd.log.opts").read_text().split() == ["--mem", "5G", "--gpu", "1"]
+
+
+def test_driver_cmd_resource_request_options(tmp_path):
+    """--job_mem / --job_gpu change the launcher's request (--job_gpu 0 drops the GPU request); the JOB
+    argv is the same either way."""
+    data = tmp_path / "data" / "dev"
+    data.mkdir(parents=True)
+    (data / "wav.scp").write_text("".join("u%d /x/u%d.wav\n" % (i, i) for i in range(4)))
+    argvs = []
+    for extra, want in ((["--job_mem", "8G"], ["--mem", "8G", "--gpu", "1"]), (["--job_gpu", "0"], ["--mem", "5G"])):
+        log = tmp_path / ("cmd%d.log" % len(argvs))
+        env = dict(os.environ, FAKE_CMD_LOG=str(log), HIP_VISIBLE_DEVICES="0,1")
+        cmd = ["bash", os.path.join(ROOT, "scripts", "make_FDLPspectrum_feats.sh"), "--nj", "2"] + extra + [
+               "--cmd", os.path.join(ROOT, "tests", "fakes", "fake_run_pl.sh"), str(data), str(tmp_path / "fbank")]
+        r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert (tmp_path / (log.name + ".opts")).read_text().split() == want
+        argvs.append(log.read_text())
+    assert argvs[0] == argvs[1]
 
 
 def test_native_cli_process_never_imports_torch(tmp_path):

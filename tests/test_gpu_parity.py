@@ -272,6 +272,32 @@ def test_lattice_durbin_matches_lds_durbin(name, monkeypatch):
         assert np.abs(a[fin] - b[fin]).max() <= TOL_UTT.get(u, 1e-6), (name, u)
 
 
+@pytest.mark.parametrize("name", ["wsj", "reverb", "mel80"])
+def test_durbin4_matches_durbin8(name):
+    """durbin4_kernel (4 lanes per item, the default for 128 <= p <= 150) against durbin8_kernel (8 lanes,
+    FDLP_LPC_LATTICE8): the same lattice recursion with the order-k dot products summed over 4 lanes x 2
+    chains instead of 8 lanes x 4 chains.  Features within 1e-6 (the ill-conditioned short2 / PESQ bands
+    as for the LDS cross-check), and a / gg of every item of a full batch at 1e-6 / 1e-9 relative."""
+    meta, sig, ref, z = load_golden(name)
+    p4, res4 = run_gpu(meta, sig, z, debug=True)
+    p8, res8 = run_gpu(meta, sig, z, debug=True, lpc="lattice8")
+    for u in meta["utts"]:
+        a, b = res4[u][0], res8[u][0]
+        fin = np.isfinite(b)
+        np.testing.assert_array_equal(np.isfinite(a), fin)
+        assert np.abs(a[fin] - b[fin]).max() <= TOL_UTT.get(u, 1e-6), (name, u)
+        assert np.abs(a - ref[u]).max() <= TOL_UTT.get(u, TOL), (name, u)
+    nf = min(64, sum(p4.geometry(sig[u].size)[0] for u in meta["utts"]))
+    d4, d8 = p4.debug_fetch(nf, keys=("a", "gg")), p8.debug_fetch(nf, keys=("a", "gg"))
+    a4, g4 = d4["a"].reshape(-1, d4["a"].shape[-1]), d4["gg"].ravel()
+    a8, g8 = d8["a"].reshape(-1, d8["a"].shape[-1]), d8["gg"].ravel()
+    assert a4.shape[0] >= 16 * 80
+    ok = np.isfinite(a8).all(axis=1) & (np.abs(a8).max(axis=1) < 1e6)
+    scale = np.abs(a8[ok]).max(axis=1, keepdims=True)
+    assert np.all(np.abs(a4[ok] - a8[ok]) <= 1e-6 * scale)
+    np.testing.assert_allclose(g4[ok], g8[ok], rtol=1e-9)
+
+
 def test_reverb_kernel_vs_oracle():
     """fdlp_reverb (preprocessing + full convolution + xcorr argmax alignment) against the oracle's
     restatement of addReverb (features.py:110-115) on random int16 signals, with and without the diff
