@@ -359,11 +359,61 @@ def spawn_ranks(n, argv):
     return next((rc for rc in rcs if rc != 0), 0)
 
 
-def run_xfer_child(args):
-    """bench.py --xfer-only in a child process with GPU_MAX_HW_QUEUES = --xfer-hw-queues; its
-    with_transfers block, or None (with the child's tail on stderr) when it fails."""
-    argv = [a for a in sys.argv[1:] if a != "--xfer-only"] + ["--xfer-only", "--no-cpu-baseline"]
-    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(args.xfer_hw_queues))
+RANK_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+            "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID")
+
+
+def xfer_child_spec(args, world, rank, local, argv=None, environ=None):
+    """argv and environment of the PCIe-pass child of one rank (started before the rank touches the GPU):
+    a single-process bench.py --xfer-only over the rank's own shard (--xfer-shard rank/world), on the rank's
+    GPU only (HIP_VISIBLE_DEVICES narrowed to it), with GPU_MAX_HW_QUEUES = --xfer-hw-queues (read once per
+    process, so the rank's own timed steps keep the default), and no rendezvous variables."""
+    argv = list(sys.argv[1:] if argv is None else argv)
+    environ = os.environ if environ is None else environ
+    out, skip = [], False
+    for a in argv:  # drop the launcher-level options the child must not inherit
+        if skip:
+            skip = False
+            continue
+        if a in ("--xfer-only", "--dry-run"):
+            continue
+        if a in ("--gpus", "--xfer-shard"):
+            skip = True
+            continue
+        if a.startswith("--gpus=") or a.startswith("--xfer-shard="):
+            continue
+        out.append(a)
+    out += ["--xfer-only", "--no-cpu-baseline", "--gpus", "1", "--xfer-shard", "%d/%d" % (rank, world)]
+    env = {k: v for k, v in environ.items() if k not in RANK_ENV}
+    env["GPU_MAX_HW_QUEUES"] = str(args.xfer_hw_queues)
+    if world > 1:
+        vis = environ.get("HIP_VISIBLE_DEVICES")
+        ids = [v.strip() for v in vis.split(",") if v.strip()] if vis else None
+        env["HIP_VISIBLE_DEVICES"] = ids[local % len(ids)] if ids else str(local)
+    return out, env
+
+
+def combine_xfer_children(got):
+    """The ranks' PCIe-pass children -> one with_transfers block: total audio over the slowest child (the
+    children run concurrently, one per GPU, but without a shared barrier); None if any child failed."""
+    if any(g is None or "audio_h" not in g for g in got):
+        return None
+    x = dict(got[0])
+    x["value"] = sum(g["audio_h"] for g in got) / max(g["elapsed_s"] for g in got)
+    x["ms_per_step"] = max(g["ms_per_step"] for g in got)
+    x["audio_h"] = sum(g["audio_h"] for g in got)
+    x["elapsed_s"] = max(g["elapsed_s"] for g in got)
+    x["per_rank_value"] = [g["value"] for g in got]
+    x.pop("mapped_output", None)
+    x["note"] = (x.get("note", "") + "; one child process per rank on its own GPU, started before the rank "
+                 "touches it, all at once: value = total audio / the slowest child's time")
+    return x
+
+
+def run_xfer_child(args, world=1, rank=0, local=0):
+    """bench.py --xfer-only in a child process (xfer_child_spec); its with_transfers block, or None (with
+    the child's tail on stderr) when it fails."""
+    argv, env = xfer_child_spec(args, world, rank, local)
     try:
         p = subprocess.run([sys.executable, os.path.abspath(__file__)] + argv, env=env, capture_output=True,
                            text=True, timeout=900)
@@ -396,10 +446,11 @@ def parse_args(argv=None):
                     help="PCIe pass: device-to-host copy streams (0: two in the child process that has its own "
                          "hardware queues, one in-process, where more streams share queues with the kernels)")
     ap.add_argument("--xfer-hw-queues", type=int, default=8,
-                    help="PCIe pass (N = 1): run it in a child process with GPU_MAX_HW_QUEUES set to this (the "
-                         "compute, H2D and D2H streams then get hardware queues of their own; 0: in-process, with "
-                         "the process default of 4)")
+                    help="PCIe pass: every rank runs it in a child process (started before the rank touches the "
+                         "GPU) with GPU_MAX_HW_QUEUES set to this (the compute, H2D and D2H streams then get hardware "
+                         "queues of their own; 0: in-process, with the process default of 4)")
     ap.add_argument("--xfer-only", action="store_true", help=argparse.SUPPRESS)  # the PCIe-pass child
+    ap.add_argument("--xfer-shard", default=None, help=argparse.SUPPRESS)  # rank/world of the child's shard
     ap.add_argument("--xfer-compute-streams", type=int, default=0,
                     help="PCIe pass: compute streams for the batches in flight (0: one per batch)")
     ap.add_argument("--pipeline", type=int, default=None, help="sub-batches over two streams (plan default 1)")
@@ -449,9 +500,11 @@ def main():
     if args.support_eps is not None:
         cfg.support_eps = args.support_eps
     probe = FdlpPlan(cfg, device=-1)
-    full = scp_list(args.workload, world, args.utts, args.seconds, args.frames, lambda t: probe.geometry(t)[0])
-    mine = shard_of(full, rank, world)
-    first = sum(split_counts(len(full), world)[:rank])
+    # the PCIe-pass child of rank r of W measures that rank's shard (same utterances as its parent)
+    s_rank, s_world = (int(v) for v in args.xfer_shard.split("/")) if args.xfer_shard else (rank, world)
+    full = scp_list(args.workload, s_world, args.utts, args.seconds, args.frames, lambda t: probe.geometry(t)[0])
+    mine = shard_of(full, s_rank, s_world)
+    first = sum(split_counts(len(full), s_world)[:s_rank])
 
     # CPU baseline first (fork before any GPU initialisation in this process), rank 0 at N=1 only
     cpu = None
@@ -459,12 +512,13 @@ def main():
         per = args.cpu_per_worker or (10 if args.config == "reverb" else 24)
         cpu = cpu_baseline(args.config, [t for _, t, _ in mine], args.cpu_workers, per, noise_host)
 
-    # PCIe-inclusive pass of a single-GPU run in a child process (before this process touches the GPU):
-    # GPU_MAX_HW_QUEUES is read once per process, and the headline keeps the process default
+    # PCIe-inclusive pass of every rank in a child process (before this process touches the GPU):
+    # GPU_MAX_HW_QUEUES is read once per process, and the headline keeps the process default.  The ranks'
+    # children run at the same time, each on its own GPU, as the JOBs of a recipe run do.
     xfer_child = None
-    if (world == 1 and not args.no_transfers and not args.dry_run and not args.xfer_only
-            and args.xfer_hw_queues > 0):
-        xfer_child = run_xfer_child(args)
+    use_child = not args.no_transfers and not args.xfer_only and args.xfer_hw_queues > 0
+    if use_child and not args.dry_run:
+        xfer_child = run_xfer_child(args, world, rank, local)
 
     if world > 1:  # host-side rendezvous: the only cross-rank traffic is a barrier and a max (no RCCL)
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -478,15 +532,25 @@ def main():
         sync = lambda: None
         elapsed = timed_steps(step, args.steps, args.warmup, sync, dist if world > 1 else None, torch.device("cpu"))
         shards = [None] * world
+        child = None
+        if use_child:
+            cargv, cenv = xfer_child_spec(args, world, rank, local)
+            child = {"argv": cargv, "env": {k: cenv.get(k) for k in ("GPU_MAX_HW_QUEUES", "HIP_VISIBLE_DEVICES")},
+                     "rank_env_dropped": not any(k in cenv for k in RANK_ENV),
+                     "before_gpu_init": "torch.cuda" not in sys.modules or not torch.cuda.is_initialized()}
+        children = [None] * world
         if world > 1:
             dist.all_gather_object(shards, [first, first + len(mine), frames])
+            dist.all_gather_object(children, child)
         else:
             shards = [[first, first + len(mine), frames]]
+            children = [child]
         if rank == 0:
             print(json.dumps({"metric": METRIC, "value": None, "unit": "audio-hours/s", "n_gpus": world,
                               "steps": args.steps, "warmup": args.warmup, "dry_run": True,
                               "config": {"workload": workload_name(args)},
-                              "scp_entries": len(full), "shards": shards, "elapsed_s": elapsed}))
+                              "scp_entries": len(full), "shards": shards, "elapsed_s": elapsed,
+                              "xfer_children": children}))
         if world > 1:
             dist.destroy_process_group()
         return
@@ -578,6 +642,10 @@ def main():
     #    and one D2H stream (--xfer-d2h-streams); the compute of batch b stays on its own stream.
     #    `mapped` = the OLA kernel stores the features straight into the pinned host buffer through its
     #    device mapping instead of a D2H copy (measured slower: reported, not used).
+    if world > 1 and use_child:  # every rank's child result, or the in-process pass on every rank
+        got = [None] * world
+        dist.all_gather_object(got, xfer_child)
+        xfer_child = combine_xfer_children(got)
     xfer = xfer_child
     if not args.no_transfers and xfer_child is None:
         pin_in = torch.from_numpy(pcm_host).pin_memory()
@@ -632,6 +700,7 @@ def main():
         mapped[0] = True
         el_m = timed_steps(xstep, args.steps, 1, sync, dd, cpu_dev)
         xfer = {"value": world * args.steps * B * audio_s / 3600.0 / el_x, "ms_per_step": el_x / args.steps * 1e3,
+                "audio_h": world * args.steps * B * audio_s / 3600.0, "elapsed_s": el_x,
                 "h2d_bytes_per_step": int(B * pcm_host.nbytes), "d2h_bytes_per_step": int(B * out.numel() * 4),
                 "mapped_output": {"value": world * args.steps * B * audio_s / 3600.0 / el_m,
                                   "ms_per_step": el_m / args.steps * 1e3,
@@ -733,6 +802,10 @@ def main():
                                 "note": "the same steps with one batch per step (stage_ms_per_step and the "
                                         "roofline are per batch, from a one-batch profiled pass)"},
         "with_transfers": xfer,
+        # SURVEY.md 8(d)'s wall "from the first H2D to the last D2H": the with_transfers pass; `value` above is
+        # the task contract's figure (PCM and features resident in HBM)
+        "sect8d_first_h2d_to_last_d2h": ({"value": xfer["value"], "unit": "audio-hours/s",
+                                          "ratio_to_value": xfer["value"] / value} if xfer else None),
         "cpu_baseline": cpu,
     }
     if rank == 0:

@@ -3,9 +3,9 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/pmck
+O=gpurun_out/${PMC_TAG:-pmck}
 mkdir -p $O
-BARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline"}
+BARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline --inflight 1 --no-transfers"}
 i=0
 for pmc in "$@"; do
   i=$((i+1))

@@ -11,7 +11,7 @@ TAG=${TAG:-r01x}
 O=gpurun_out/evidence_$TAG
 mkdir -p $O
 # one batch in flight for the trace and PMC passes: the kernels alone, as in the bench line's roofline pass
-BARGS=${BENCH_ARGS:-"--steps 5 --warmup 1 --no-cpu-baseline --inflight 1"}
+BARGS=${BENCH_ARGS:-"--steps 5 --warmup 1 --no-cpu-baseline --inflight 1 --no-transfers"}
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3 bench.py $BARGS > $O/trace.log 2>&1 || { echo "trace failed"; tail -20 $O/trace.log; exit 3; }
 python3 scripts/rocpd_summary.py $O/trace/run_results.db $O/kernel_trace_stats.csv > /dev/null || true
 i=0

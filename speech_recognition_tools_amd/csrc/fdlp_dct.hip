@@ -448,15 +448,26 @@ __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const doub
 //    Pass-3 tasks are laid out so the task holding X[M - k] sits in the adjacent lane (lane ^ 1): the
 //    unpack takes it by DPP quad_perm.  No Z intermediate in HBM: the frame is read once and D written
 //    once (the four-step pair above moves Z = 384 KB per frame through HBM).
+//    Persistent workgroups (one per CU, LDS-bound): the tables are staged once, and the next frame's
+//    descriptor and int16 samples are loaded during the current frame's passes 2-3, its window during
+//    the current frame's row writes, so the gather latency (14 of 40 us per frame, r03am) is hidden.
+//    The LDS images are padded (exchange 1: k1 stride 601 = 25 mod 32; exchange 2: k2a stride 529) and
+//    the twiddle tables laid out [k1][t mod 16] x [k1][t div 16] and [k2a][q3], so the lanes of an LDS
+//    instruction spread over the banks (benchmarks/dct_lds_model.py).
 // -----------------------------------------------------------------------------------------
 namespace dct1 {
 constexpr int kA = 20, kB = 24, kC = 25, kM = kA * kB * kC, kBC = kB * kC, kAC = kA * kC, kAB = kA * kB;
 constexpr int kThreads = 640;  // >= max(BC, AC, AB) tasks
 static_assert(kM == 12000 && kBC <= kThreads && kAC <= kThreads && kAB <= kThreads, "task layout");
-// table offsets (double2) in c.dct1_tw / LDS: W_M^b (b < BC), W_A^a, W_BC^e, rtw[lo], rtw[AB h],
-// post[lo], post[AB h]  (lo < AB, h < C)
-constexpr int kTwM = 0, kTwA = kTwM + kBC, kTwBC = kTwA + kA, kRtLo = kTwBC + kBC, kRtHi = kRtLo + kAB,
+constexpr int kT2N = (kBC + 15) / 16;  // t div 16 < 38
+// table offsets (double2) in c.dct1_tw / LDS: T1[k1][u] = W_M^{k1 u} (u < 16), T2[k1][v] = W_M^{16 k1 v}
+// (v < 38), T3[k2a][q3] = W_BC^{k2a q3}, rtw[lo], rtw[AB h], post[lo], post[AB h]  (lo < AB, h < C)
+constexpr int kT1 = 0, kT2 = kT1 + kA * 16, kT3 = kT2 + kA * kT2N, kRtLo = kT3 + kB * kC, kRtHi = kRtLo + kAB,
               kPwLo = kRtHi + kC, kPwHi = kPwLo + kAB, kTabs = kPwHi + kC;
+// exchange images (doubles): [k1][n2] with k1 stride kQ1, [k2a][k1][q3] with k2a stride kP2
+constexpr int kQ1 = 601, kP2 = 529;
+constexpr int kXch0 = kA * kQ1 > (kB - 1) * kP2 + kAC ? kA * kQ1 : (kB - 1) * kP2 + kAC;
+constexpr int kXch = ((kXch0 > kM ? kXch0 : kM) + 15) / 16 * 16;
 
 // cos / sin of 2 pi e / n, evaluated by the compiler (Taylor series on [0, pi/4] after an exact
 // integer quadrant / octant reduction); used for the in-register radix twiddles
@@ -565,269 +576,237 @@ __device__ __forceinline__ void pass3_task(int t, int& k1, int& k2a, int& mode) 
 }
 }  // namespace dct1
 
-#ifndef FDLP_DCT_PREFETCH
-#define FDLP_DCT_PREFETCH 0  // 1: L2 prefetch of the PCM of the frame 256 workgroups ahead (A/B builds)
-#endif
-#ifndef FDLP_DCT_PHASES
-#define FDLP_DCT_PHASES 0  // 1 / 2: timing builds only - thread 0 overwrites D[f][0..9] with phase timestamps
-#endif
+// Frames of the fast gather: int16 PCM without noise or the diff filter whose reflect padding
+// (numpy 'reflect', features.py:146) is at most one bounce, sample u -> -u below 0 and 2(T-1) - u from T on
+// (every frame of an utterance longer than the half window; the others take the general gather).
+__device__ __forceinline__ bool dct1_fast(const DevConsts& c, const FrameDesc& fd, int pcm_kind) {
+  const int64_t t0 = (int64_t)fd.k * c.hop - c.ext;
+  return pcm_kind == 0 && fd.noise_off < 0 && fd.T >= 2 && t0 >= -(fd.T - 1) &&
+         t0 + 2 * dct1::kM - 1 <= 2 * (fd.T - 1);
+}
+
+// Two frames per workgroup (f = 2 b, 2 b + 1), as straight-line code: the tables are staged once per two
+// frames.  (A persistent loop over frames spills: the register allocator keeps ~60 more registers live
+// around the loop's back edge than through the same code twice; so does a prefetch of the second frame's
+// gather into registers during the first frame, at 640 threads = 168 VGPRs.)
+constexpr int kDctFramesPerBlock = 2;
+
 __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, const void* __restrict__ pcm,
                                                                    int pcm_kind, const int16_t* __restrict__ noise,
                                                                    const FrameDesc* __restrict__ frames,
                                                                    const double* __restrict__ dense_rows,
-                                                                   double scale2, double* __restrict__ dct) {
+                                                                   int nframes, double scale2,
+                                                                   double* __restrict__ dct) {
   using namespace dct1;
-  __shared__ __attribute__((aligned(16))) double xch[kM];
+  __shared__ __attribute__((aligned(16))) double xch[kXch];
   __shared__ double2 tab[kTabs + kC];  // tables + the (0, 0) task's X (pass 3)
   const int t = threadIdx.x;
-  const int f = blockIdx.x;
   constexpr int N = 2 * kM;
-#if FDLP_DCT_PHASES
-  long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  long long tg[4] = {0, 0, 0, 0};  // FDLP_DCT_PHASES == 2: gather / tables / radix-20 split of phase 0
-  if (t == 0) ts[0] = wall_clock64();
-#endif
+  const double2* hwin = c.dct1_tw + kTabs;  // the window in Makhoul order (dct_frame_tables)
 
-  // ---- pass 1: thread n2 = C q2 + q3 gathers z[BC q1 + n2] = v[2q] + i v[2q+1] (Makhoul order) ----
-  double2 y1[kA];
-  if (t < kBC && !dense_rows) {
-    const FrameDesc fd = frames[f];
-    const int64_t t0 = (int64_t)fd.k * c.hop - c.ext;
-    const bool fast = pcm_kind == 0 && fd.noise_off < 0 && t0 >= 0 && t0 + N <= fd.T;
-    if (fast) {
-      const int16_t* xs = (const int16_t*)pcm + fd.pcm_off + t0;
-      const double2* hwin = c.dct1_tw + kTabs;  // the window in Makhoul order (dct_frame_tables)
+  // the fast gather: thread n2 = C q2 + q3 takes the int16 pair (x[m0], x[m1]) of the packed samples
+  // z[BC q1 + n2] = v[2q] + i v[2q+1] (v[2q] = x[4q], v[2q+1] = x[4q+2] in the first half, mirrored
+  // (x[2N-1-4q], x[2N-3-4q]) after; frame positions reflected into the utterance) into one register (two
+  // 16-bit loads), and the window pair (w[m0], w[m1]) (one coalesced 16-byte load)
+  // (two int16 per register by 16-bit loads into the halves would halve the registers of a prefetch, but
+  // gfx950 runs with SRAM ECC, where a D16 load does not preserve the other half of its register)
+  auto load_samples = [&](int (&pk)[2 * kA], int fi) {
+    const FrameDesc fd = frames[fi];
+    const int16_t* xs = (const int16_t*)pcm + fd.pcm_off;  // the utterance
+    const int t0 = (int)((int64_t)fd.k * c.hop - c.ext), T = fd.T;
 #pragma unroll
-      for (int q1 = 0; q1 < kA; ++q1) {
-        const int q = kBC * q1 + t;
-        // v[2q] = x[4q], v[2q+1] = x[4q+2] in the first half, mirrored (x[2N-1-4q], x[2N-3-4q]) after
-        const int m0 = 4 * q1 < kA * 2 ? 4 * q : 2 * N - 1 - 4 * q;
-        const int m1 = 4 * q1 < kA * 2 ? 4 * q + 2 : 2 * N - 3 - 4 * q;
-        const double2 hw = hwin[q];  // (hamming[m0], hamming[m1]): one coalesced 16-byte load
-        y1[q1].x = __dmul_rn((double)xs[m0], hw.x);
-        y1[q1].y = __dmul_rn((double)xs[m1], hw.y);
-      }
+    for (int q1 = 0; q1 < kA; ++q1) {
+      const int q = kBC * q1 + t;
+      int u0 = t0 + (4 * q1 < kA * 2 ? 4 * q : 2 * N - 1 - 4 * q);
+      int u1 = t0 + (4 * q1 < kA * 2 ? 4 * q + 2 : 2 * N - 3 - 4 * q);
+      u0 = u0 < 0 ? -u0 : (u0 >= T ? 2 * (T - 1) - u0 : u0);
+      u1 = u1 < 0 ? -u1 : (u1 >= T ? 2 * (T - 1) - u1 : u1);
+      pk[2 * q1] = xs[u0];
+      pk[2 * q1 + 1] = xs[u1];
     }
-  }
-  // general frames (reflect padding, noise mixing, the diff filter, fp64 input, dense rows): the
-  // samples are staged through xch by a rolled loop (the general gather is too large to unroll 40x),
-  // real parts then imaginary parts; the branch is uniform over the workgroup
-  const bool fast_wg = !dense_rows && pcm_kind == 0 && [&] {
-    const FrameDesc fd0 = frames[f];
-    const int64_t s0 = (int64_t)fd0.k * c.hop - c.ext;
-    return fd0.noise_off < 0 && s0 >= 0 && s0 + N <= fd0.T;
-  }();
-  if (!fast_wg) {
-    FrameDesc fd;
-    if (!dense_rows) fd = frames[f];
+  };
+  auto load_window = [&](double2 (&wv)[kA]) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      for (int q = t; q < kM; q += kThreads) xch[q] = makhoul_sample(c, fd, 2 * q + h, f, pcm, pcm_kind, noise, dense_rows);
-      __syncthreads();
+    for (int q1 = 0; q1 < kA; ++q1) wv[q1] = hwin[kBC * q1 + t];
+  };
+
+  const int f0 = kDctFramesPerBlock * (int)blockIdx.x;
+  for (int q = t; q < kTabs; q += kThreads) tab[q] = c.dct1_tw[q];
+  __syncthreads();  // tables
+
+  auto frame = [&](const int f) {
+    const bool fast = !dense_rows && dct1_fast(c, frames[f], pcm_kind);
+    // ---- pass 1: thread n2 = C q2 + q3 holds z[BC q1 + n2] (Makhoul order) ----
+    double2 y1[kA];
+    if (fast) {
       if (t < kBC) {
+        int pk[2 * kA];
+        load_samples(pk, f);
+        load_window(y1);
 #pragma unroll
         for (int q1 = 0; q1 < kA; ++q1) {
-          const double v = xch[kBC * q1 + t];
-          if (h) y1[q1].y = v; else y1[q1].x = v;
+          y1[q1].x = __dmul_rn((double)pk[2 * q1], y1[q1].x);
+          y1[q1].y = __dmul_rn((double)pk[2 * q1 + 1], y1[q1].y);
+        }
+      }
+    } else {
+      // general frames (multi-bounce reflect padding, noise mixing, the diff filter, fp64 input, dense rows):
+      // the samples are staged through xch by a rolled loop (the general gather is too large to unroll 40x),
+      // real parts then imaginary parts; the branch is uniform over the workgroup
+      FrameDesc fd;
+      if (!dense_rows) fd = frames[f];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        for (int q = t; q < kM; q += kThreads) xch[q] = makhoul_sample(c, fd, 2 * q + h, f, pcm, pcm_kind, noise, dense_rows);
+        __syncthreads();
+        if (t < kBC) {
+#pragma unroll
+          for (int q1 = 0; q1 < kA; ++q1) {
+            const double v = xch[kBC * q1 + t];
+            if (h) y1[q1].y = v; else y1[q1].x = v;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    if (t < kBC) {
+      rdft<kA>(y1);
+#pragma unroll
+      for (int k1 = 1; k1 < kA; ++k1)  // W_M^{k1 n2} = W_M^{k1 (n2 mod 16)} W_M^{16 k1 (n2 div 16)}
+        y1[k1] = cmul(y1[k1], cmul(tab[kT1 + 16 * k1 + (t & 15)], tab[kT2 + kT2N * k1 + (t >> 4)]));
+    }
+    // ---- exchange 1: [k1][n2] -> thread (k1, q3) reads q2 ----
+    const int k1b = t / kC, q3 = t - kC * (t / kC);
+    double2 y2[kB];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (t < kBC) {
+#pragma unroll
+        for (int k1 = 0; k1 < kA; ++k1) xch[k1 * kQ1 + t] = h ? y1[k1].y : y1[k1].x;
+      }
+      __syncthreads();
+      if (t < kAC) {
+#pragma unroll
+        for (int q2 = 0; q2 < kB; ++q2) {
+          const double v = xch[k1b * kQ1 + kC * q2 + q3];
+          if (h) y2[q2].y = v; else y2[q2].x = v;
         }
       }
       __syncthreads();
     }
-  }
-  // the tables after the sample gather: their loads overlap the gather's instead of preceding them
-#if FDLP_DCT_PHASES == 2
-  if (t == 0) {
-    // thread 0's gathered samples are in registers: wait for them (timing build only)
-    for (int q1 = 0; q1 < kA; ++q1) asm volatile("" ::"v"(y1[q1].x), "v"(y1[q1].y));
-    tg[0] = wall_clock64();
-  }
-#endif
-  for (int q = t; q < kTabs; q += kThreads) tab[q] = c.dct1_tw[q];
-#if FDLP_DCT_PREFETCH
-  // L2 prefetch of the frame kPf ahead (a multiple of 8 workgroups: the same XCD, which runs it about one
-  // round of workgroups later): one int16 load per 80 bytes touches every line of its 48 KB of PCM.
-  // Issued after this frame's gather and table loads, so no wait of this workgroup includes it (the
-  // exchanges and passes below issue no vector loads); its value is kept alive to the kernel's end.
-  int pf_keep = 0;
-  {
-    constexpr int kPf = 256;
-    const int fp = f + kPf;
-    if (fp < (int)gridDim.x && !dense_rows && pcm_kind == 0 && 40 * t < N) {
-      const FrameDesc fdp = frames[fp];
-      const int64_t s0 = (int64_t)fdp.k * c.hop - c.ext;
-      if (s0 >= 0 && s0 + N <= fdp.T) pf_keep = ((const int16_t*)pcm)[fdp.pcm_off + s0 + 40 * t];
-    }
-  }
-#endif
-#if FDLP_DCT_PHASES == 2
-  if (t == 0) tg[1] = wall_clock64();
-#endif
-  if (t < kBC) rdft<kA>(y1);
-#if FDLP_DCT_PHASES == 2
-  if (t == 0) {
-    for (int q1 = 0; q1 < kA; ++q1) asm volatile("" ::"v"(y1[q1].x), "v"(y1[q1].y));
-    tg[2] = wall_clock64();
-  }
-#endif
-  __syncthreads();  // tables
-#if FDLP_DCT_PHASES
-  if (threadIdx.x == 0) ts[1] = wall_clock64();
-#endif
-  if (t < kBC) {
+    // ---- pass 2: DFT_B over q2, twiddle W_BC^{k2a q3}; exchange 2: [k2a][k1][q3] ----
+    if (t < kAC) {
+      rdft<kB>(y2);
 #pragma unroll
-    for (int k1 = 1; k1 < kA; ++k1) {  // W_M^{k1 n2}, k1 n2 = BC a + b: W_A^a W_M^b
-      const int e = k1 * t, a = e / kBC, b = e - kBC * a;
-      y1[k1] = cmul(y1[k1], cmul(tab[kTwA + a], tab[kTwM + b]));
+      for (int k2a = 1; k2a < kB; ++k2a) y2[k2a] = cmul(y2[k2a], tab[kT3 + kC * k2a + q3]);
     }
-  }
-  // ---- exchange 1: [k1][n2] -> thread (k1, q3) reads q2 ----
-  const int k1b = t / kC, q3 = t - kC * (t / kC);
-  double2 y2[kB];
+    int k1, k2a, mode;
+    dct1::pass3_task(t < kAB ? t : 0, k1, k2a, mode);
+    double2 y3[kC];
+    const int a3 = k2a * kP2 + k1 * kC;
+    if (t < kAC) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (t < kBC) {
-#pragma unroll
-      for (int k1 = 0; k1 < kA; ++k1) xch[k1 * kBC + t] = h ? y1[k1].y : y1[k1].x;
+      for (int j = 0; j < kB; ++j) xch[j * kP2 + t] = y2[j].x;
     }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kC; ++j) y3[j].x = xch[a3 + j];
     __syncthreads();
     if (t < kAC) {
 #pragma unroll
-      for (int q2 = 0; q2 < kB; ++q2) {
-        const double v = xch[k1b * kBC + kC * q2 + q3];
-        if (h) y2[q2].y = v; else y2[q2].x = v;
-      }
+      for (int j = 0; j < kB; ++j) xch[j * kP2 + t] = y2[j].y;
     }
     __syncthreads();
-  }
-  // ---- pass 2: DFT_B over q2, twiddle W_BC^{k2a q3}; exchange 2: [k2a][k1][q3] ----
-#if FDLP_DCT_PHASES
-  if (threadIdx.x == 0) ts[2] = wall_clock64();
-#endif
-  if (t < kAC) {
-    rdft<kB>(y2);
 #pragma unroll
-    for (int k2a = 1; k2a < kB; ++k2a) y2[k2a] = cmul(y2[k2a], tab[kTwBC + k2a * q3]);
-  }
-  int k1, k2a, mode;
-#if FDLP_DCT_PHASES
-  if (threadIdx.x == 0) ts[3] = wall_clock64();
-#endif
-  dct1::pass3_task(t < kAB ? t : 0, k1, k2a, mode);
-  double2 y3[kC];
-  const int a3 = k2a * kAC + k1 * kC;
-  if (t < kAC) {
-#pragma unroll
-    for (int j = 0; j < kB; ++j) xch[j * kAC + t] = y2[j].x;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kC; ++j) y3[j].x = xch[a3 + j];
-  __syncthreads();
-  if (t < kAC) {
-#pragma unroll
-    for (int j = 0; j < kB; ++j) xch[j * kAC + t] = y2[j].y;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kC; ++j) y3[j].y = xch[a3 + j];
-  // ---- pass 3: DFT_C over q3 -> X[k1 + A k2a + AB k2b]; unpack with X[M - k] ----
-  // D leaves through LDS: the lanes' D[k] (k = lo + AB j: 8-byte pieces scattered over the row, 1.44x
-  // the row's bytes in partial-line writes, r03e PMC) are staged in xch, then every thread of the
-  // workgroup writes contiguous 16-byte pieces of the row; first D[0, M), then D[M, 2M) (held in
-  // registers meanwhile).  The waves without pass-3 tasks stay for the barriers and the row writes.
-  const bool task3 = t < kAB;
-  if (task3) rdft<kC>(y3);
-#if FDLP_DCT_PHASES
-  if (threadIdx.x == 0) ts[4] = wall_clock64();
-#endif
-  const int lo = k1 + kA * k2a;
-  double2 rl = make_double2(0.0, 0.0), pl = rl;
-  if (task3) {
-    rl = tab[kRtLo + lo];
-    pl = tab[kPwLo + lo];
-  }
-  double* drow = dct + (int64_t)f * N;
-  double dhi[kC];  // D[k + M] of the lane's k = lo + AB j
-#pragma unroll
-  for (int j = 0; j < kC; ++j) dhi[j] = 0.0;
-  // the one lane of task (0, 0) pairs X_k with its own X_{M-k} (register (C - j) mod C): it parks its X
-  // in LDS, and 25 lanes of an otherwise idle wave (t = 512 ..) emit one output pair each (done by that
-  // lane alone, its 25 outputs ran after everyone else's while the workgroup waited at the barrier)
-  if (task3 && mode == 1) {
-#pragma unroll
-    for (int j = 0; j < kC; ++j) tab[kTabs + j] = y3[j];
-  }
-  const int hj = t - 8 * 64;
-  const bool helper = hj >= 0 && hj < kC;
-  static_assert(kThreads >= 8 * 64 + kC && kAB <= 8 * 64, "helper lanes of task (0, 0)");
-  __syncthreads();  // every lane's pass-3 reads of xch are done; the (0, 0) values are parked
-  // D[k], D[k + M] from V = X_k and W = X_{M-k} (E / O split of the packed FFT, Makhoul post-twiddle)
-  auto emit_pair = [&](int j, double2 V, double2 W, double2 rlo, double2 plo, double& d1, double& d2) {
-    const double2 E = make_double2(0.5 * (V.x + W.x), 0.5 * (V.y - W.y));
-    const double2 O = make_double2(0.5 * (V.y + W.y), -0.5 * (V.x - W.x));
-    const double2 rt = cmul(rlo, tab[kRtHi + j]);
-    const double2 w1 = cmul(plo, tab[kPwHi + j]);
-    constexpr double hr = 0.70710678118654752440;  // post[k + M] = post[k] e^{-i pi / 4}
-    const double2 w2 = make_double2(hr * (w1.x + w1.y), hr * (w1.y - w1.x));
-    const double2 tt = cmul(rt, O);
-    const double2 V1 = make_double2(E.x + tt.x, E.y + tt.y);
-    const double2 V2 = make_double2(E.x - tt.x, E.y - tt.y);
-    d1 = (w1.x * V1.x - w1.y * V1.y) * scale2;
-    d2 = (w2.x * V2.x - w2.y * V2.y) * scale2;
-  };
-  auto emit = [&](int j, double2 V, double2 W) {
-    double d1, d2;
-    emit_pair(j, V, W, rl, pl, d1, d2);
-    xch[lo + kAB * j] = d1;
-    dhi[j] = d2;
-  };
-  // pairs in lanes (2i, 2i+1) and the self-paired (0, 12) (mode 2): X_{M-k} is register C-1-j of the
-  // partner lane, or of the lane itself
-  const bool act = task3 && mode != 1;
-  // j and C-1-j together, so both registers are dead after the pair (C odd: the middle one alone)
-#pragma unroll
-  for (int j = 0; j < (kC + 1) / 2; ++j) {
-    const int jm = kC - 1 - j;
-    const double2 a = y3[j], b = y3[jm];
-    const double2 sa = swap_pair(a), sb = swap_pair(b);  // every lane of the wave takes part in the DPP
-    if (act) {
-      emit(j, a, mode == 2 ? b : sb);
-      if (jm != j) emit(jm, b, mode == 2 ? a : sa);
+    for (int j = 0; j < kC; ++j) y3[j].y = xch[a3 + j];
+    // ---- pass 3: DFT_C over q3 -> X[k1 + A k2a + AB k2b]; unpack with X[M - k] ----
+    // D leaves through LDS: the lanes' D[k] (k = lo + AB j: 8-byte pieces scattered over the row, 1.44x
+    // the row's bytes in partial-line writes, r03e PMC) are staged in xch, then every thread of the
+    // workgroup writes contiguous 16-byte pieces of the row; first D[0, M), then D[M, 2M) (held in
+    // registers meanwhile).  The waves without pass-3 tasks stay for the barriers and the row writes.
+    const bool task3 = t < kAB;
+    if (task3) rdft<kC>(y3);
+    const int lo = k1 + kA * k2a;
+    double2 rl = make_double2(0.0, 0.0), pl = rl;
+    if (task3) {
+      rl = tab[kRtLo + lo];
+      pl = tab[kPwLo + lo];
     }
-  }
-  double dh_help = 0.0;
-  if (helper) {  // task (0, 0), output pair hj: X_{AB hj} and X_{M - AB hj} = X_{AB ((C - hj) mod C)}
-    double d1;
-    emit_pair(hj, tab[kTabs + hj], tab[kTabs + (kC - hj) % kC], tab[kRtLo], tab[kPwLo], d1, dh_help);
-    xch[kAB * hj] = d1;
-  }
-  // row writes: 16-byte pieces, consecutive threads on consecutive pieces (M / 2 = 6000 per half)
-  double2* drow2 = reinterpret_cast<double2*>(drow);
-  const double2* xch2 = reinterpret_cast<const double2*>(xch);
-  __syncthreads();
-#if FDLP_DCT_PHASES
-  if (threadIdx.x == 0) ts[5] = wall_clock64();
-#endif
-  for (int q = t; q < kM / 2; q += kThreads) drow2[q] = xch2[q];
-  __syncthreads();
-  if (act) {
+    double* drow = dct + (int64_t)f * N;
+    double dhi[kC];  // D[k + M] of the lane's k = lo + AB j
 #pragma unroll
-    for (int j = 0; j < kC; ++j) xch[lo + kAB * j] = dhi[j];
+    for (int j = 0; j < kC; ++j) dhi[j] = 0.0;
+    // the one lane of task (0, 0) pairs X_k with its own X_{M-k} (register (C - j) mod C): it parks its X
+    // in LDS, and 25 lanes of an otherwise idle wave (t = 512 ..) emit one output pair each (done by that
+    // lane alone, its 25 outputs ran after everyone else's while the workgroup waited at the barrier)
+    if (task3 && mode == 1) {
+#pragma unroll
+      for (int j = 0; j < kC; ++j) tab[kTabs + j] = y3[j];
+    }
+    const int hj = t - 8 * 64;
+    const bool helper = hj >= 0 && hj < kC;
+    static_assert(kThreads >= 8 * 64 + kC && kAB <= 8 * 64, "helper lanes of task (0, 0)");
+    __syncthreads();  // every lane's pass-3 reads of xch are done; the (0, 0) values are parked
+    // D[k], D[k + M] from V = X_k and W = X_{M-k} (E / O split of the packed FFT, Makhoul post-twiddle)
+    auto emit_pair = [&](int j, double2 V, double2 W, double2 rlo, double2 plo, double& d1, double& d2) {
+      const double2 E = make_double2(0.5 * (V.x + W.x), 0.5 * (V.y - W.y));
+      const double2 O = make_double2(0.5 * (V.y + W.y), -0.5 * (V.x - W.x));
+      const double2 rt = cmul(rlo, tab[kRtHi + j]);
+      const double2 w1 = cmul(plo, tab[kPwHi + j]);
+      constexpr double hr = 0.70710678118654752440;  // post[k + M] = post[k] e^{-i pi / 4}
+      const double2 w2 = make_double2(hr * (w1.x + w1.y), hr * (w1.y - w1.x));
+      const double2 tt = cmul(rt, O);
+      const double2 V1 = make_double2(E.x + tt.x, E.y + tt.y);
+      const double2 V2 = make_double2(E.x - tt.x, E.y - tt.y);
+      d1 = (w1.x * V1.x - w1.y * V1.y) * scale2;
+      d2 = (w2.x * V2.x - w2.y * V2.y) * scale2;
+    };
+    auto emit = [&](int j, double2 V, double2 W) {
+      double d1, d2;
+      emit_pair(j, V, W, rl, pl, d1, d2);
+      xch[lo + kAB * j] = d1;
+      dhi[j] = d2;
+    };
+    // pairs in lanes (2i, 2i+1) and the self-paired (0, 12) (mode 2): X_{M-k} is register C-1-j of the
+    // partner lane, or of the lane itself
+    const bool act = task3 && mode != 1;
+    // j and C-1-j together, so both registers are dead after the pair (C odd: the middle one alone)
+#pragma unroll
+    for (int j = 0; j < (kC + 1) / 2; ++j) {
+      const int jm = kC - 1 - j;
+      const double2 a = y3[j], b = y3[jm];
+      const double2 sa = swap_pair(a), sb = swap_pair(b);  // every lane of the wave takes part in the DPP
+      if (act) {
+        emit(j, a, mode == 2 ? b : sb);
+        if (jm != j) emit(jm, b, mode == 2 ? a : sa);
+      }
+    }
+    double dh_help = 0.0;
+    if (helper) {  // task (0, 0), output pair hj: X_{AB hj} and X_{M - AB hj} = X_{AB ((C - hj) mod C)}
+      double d1;
+      emit_pair(hj, tab[kTabs + hj], tab[kTabs + (kC - hj) % kC], tab[kRtLo], tab[kPwLo], d1, dh_help);
+      xch[kAB * hj] = d1;
+    }
+    // row writes: 16-byte pieces, consecutive threads on consecutive pieces (M / 2 = 6000 per half)
+    double2* drow2 = reinterpret_cast<double2*>(drow);
+    const double2* xch2 = reinterpret_cast<const double2*>(xch);
+    __syncthreads();
+    for (int q = t; q < kM / 2; q += kThreads) drow2[q] = xch2[q];
+    __syncthreads();
+    if (act) {
+#pragma unroll
+      for (int j = 0; j < kC; ++j) xch[lo + kAB * j] = dhi[j];
+    }
+    if (helper) xch[kAB * hj] = dh_help;
+    __syncthreads();
+    for (int q = t; q < kM / 2; q += kThreads) drow2[kM / 2 + q] = xch2[q];
+  };
+
+  frame(f0);
+  if (f0 + 1 < nframes) {
+    __syncthreads();  // the row reads of xch before the second frame's exchanges
+    frame(f0 + 1);
   }
-  if (helper) xch[kAB * hj] = dh_help;
-  __syncthreads();
-  for (int q = t; q < kM / 2; q += kThreads) drow2[kM / 2 + q] = xch2[q];
-#if FDLP_DCT_PREFETCH
-  asm volatile("" ::"v"(pf_keep));
-#endif
-#if FDLP_DCT_PHASES
-  __syncthreads();
-  if (t == 0) {
-    ts[6] = wall_clock64();
-    for (int i = 0; i < 7; ++i) drow[i] = (double)ts[i];
-    for (int i = 0; i < 3; ++i) drow[7 + i] = (double)tg[i];
-  }
-#endif
 }
 
 // host tables of dct_frame_kernel (double2 [dct1::kTabs]); empty unless N = 24000 with the real FFT
@@ -851,9 +830,12 @@ std::vector<double2> dct_frame_tables(int N, const std::vector<double>& window) 
     const long double ang = -PI * (long double)k / (2.0L * (long double)N);
     return make_double2((double)cosl(ang), (double)sinl(ang));
   };
-  for (int b = 0; b < kBC; ++b) tab[kTwM + b] = root(b, kM);
-  for (int a = 0; a < kA; ++a) tab[kTwA + a] = root(a, kA);
-  for (int e = 0; e < kBC; ++e) tab[kTwBC + e] = root(e, kBC);
+  for (int k1 = 0; k1 < kA; ++k1) {
+    for (int u = 0; u < 16; ++u) tab[kT1 + 16 * k1 + u] = root((long long)k1 * u, kM);
+    for (int v = 0; v < kT2N; ++v) tab[kT2 + kT2N * k1 + v] = root(16LL * k1 * v, kM);
+  }
+  for (int k2a = 0; k2a < kB; ++k2a)
+    for (int q3 = 0; q3 < kC; ++q3) tab[kT3 + kC * k2a + q3] = root((long long)k2a * q3, kBC);
   for (int lo = 0; lo < kAB; ++lo) { tab[kRtLo + lo] = root(lo, N); tab[kPwLo + lo] = post(lo); }
   for (int h = 0; h < kC; ++h) { tab[kRtHi + h] = root((long long)kAB * h, N); tab[kPwHi + h] = post((long long)kAB * h); }
   return tab;
@@ -865,8 +847,9 @@ hipError_t launch_dct_frame(const DevConsts& c, const void* pcm, int pcm_kind, c
   if (nframes <= 0) return hipSuccess;
   if (!c.dct1_tw || c.N != 2 * dct1::kM || !c.real_fft || c.natural) return hipErrorInvalidValue;
   const double sc2 = 2.0 / sqrt((double)(2 * c.N));
-  hipLaunchKernelGGL(dct_frame_kernel, dim3(nframes), dim3(dct1::kThreads), 0, s, c, pcm, pcm_kind, noise, frames,
-                     dense_rows, sc2, dct);
+  const int grid = (nframes + kDctFramesPerBlock - 1) / kDctFramesPerBlock;
+  hipLaunchKernelGGL(dct_frame_kernel, dim3(grid), dim3(dct1::kThreads), 0, s, c, pcm, pcm_kind, noise, frames,
+                     dense_rows, nframes, sc2, dct);
   return hipGetLastError();
 }
 

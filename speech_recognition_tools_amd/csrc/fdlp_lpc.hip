@@ -739,9 +739,9 @@ __global__ __launch_bounds__(64, 2) void durbin8_kernel(const double* __restrict
 // * 1/E for the next order (rcp + two Newton steps) is computed right after kappa, beside the order's
 //   FMAs, so the serial part of an order is only the dot-product tail, the quad sum and kappa.
 // * No r staging: R1 is re-laid out with A through the item's LDS image (R1 first, while B is already
-//   dead), the 8 positions a phase adds come from global loads issued one phase ahead.  16 items x 156
-//   doubles = 19.6 KB of LDS per wave, two waves per SIMD.
-// Phases S = 1, 3, 5, ... (odd: the lane strides S and S + 2 with the item stride 156 = -4 mod 32 doubles
+//   dead), the 16 positions a phase adds come from global loads issued one phase ahead.  16 items x 156
+//   doubles = 19.7 KB of LDS per wave, two waves per SIMD.
+// Phases S = 1, 5, 9, ... (odd: the lane strides S and S + 4 with the item stride 156 = -4 mod 32 doubles
 // put the 32 lanes of a ds_read_b64 group and the 16 of a ds_write_b64 group on distinct banks), then SL4.
 // Same recursion and the same kappa / E / 1/E arithmetic as c8_step (features.py:226-228); the order-k dot
 // product is summed over 4 lane partials of 2 chains instead of 8 lanes of 4 chains.
@@ -784,12 +784,15 @@ __device__ __forceinline__ void c4_step(double (&A)[S], double (&B)[S], const do
   rE = rcp_newton(E);
 }
 
-// LDS doubles per item: the image of 4 S positions plus the 8 a phase adds, = 28 mod 32 (see above)
+// Phases S = 1, 1 + kC4Step, ... (16 orders each), then SL4: a relayout every 16 orders (every 8 with
+// step 2: 19 instead of 11 relayouts for p = 150, 1.8x the LDS instructions) for ~1 more padded slot
+// per lane.  LDS doubles per item: the image of 4 SL4 positions, = 28 mod 32 (see above).
+constexpr int kC4Step = 4;
 __host__ __device__ constexpr int c4_item_stride(int SL4) {
-  const int need = 4 * (SL4 - 1) + 8 > 4 * SL4 ? 4 * (SL4 - 1) + 8 : 4 * SL4;
+  const int need = 4 * SL4;
   return need + ((28 - need % 32) + 32) % 32;
 }
-constexpr int kC4Guard = 16;  // doubles below item 0's image (the mirrored B reads reach index -9)
+constexpr int kC4Guard = 24;  // doubles below item 0's image (the mirrored B reads reach index -4 kC4Step - 1)
 
 // Orders [k0, min(p, 4 S - 2)] of phase S, then the next phase.  Returns (in cap) 4 S of the phase that
 // ends at order p and leaves its A in img (positions < cap; exactly 0 past p), gg in g.
@@ -798,13 +801,16 @@ __device__ __forceinline__ void c4_durbin(double (&A)[S], double (&B)[S], double
                                           double& rE, double* img, const double* rrow, int p, int li, bool valid,
                                           double r0, int k0, int& cap, double& g) {
   const int k1 = min(p, 4 * S - 2);
-  constexpr int SN = S + 2 <= SL4 ? S + 2 : SL4;
-  double rn[2] = {0.0, 0.0};  // R1 of the 8 positions the next phase adds: 4 S + 2 li + t
+  constexpr int SN = S + kC4Step <= SL4 ? S + kC4Step : SL4;
+  constexpr int NA = SN > S ? SN - S : 1;  // positions per lane the next phase adds
+  double rn[NA];  // R1 of the 4 NA positions the next phase adds: 4 S + li + 4 t (lanes on distinct banks)
+#pragma unroll
+  for (int t = 0; t < NA; ++t) rn[t] = 0.0;
   if constexpr (SN > S) {
     if (k1 < p) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int m = 4 * S + 2 * li + t;
+      for (int t = 0; t < NA; ++t) {
+        const int m = 4 * S + li + 4 * t;
         if (valid && m <= p) rn[t] = rrow[m + 1];
       }
     }
@@ -817,8 +823,8 @@ __device__ __forceinline__ void c4_durbin(double (&A)[S], double (&B)[S], double
       wave_lds_sync();
 #pragma unroll
       for (int j = 0; j < S; ++j) img[li * S + j] = R1[j];
-      img[4 * S + 2 * li] = rn[0];
-      img[4 * S + 2 * li + 1] = rn[1];
+#pragma unroll
+      for (int t = 0; t < NA; ++t) img[4 * S + li + 4 * t] = rn[t];
       wave_lds_sync();
 #pragma unroll
       for (int j = 0; j < SN; ++j) R1n[j] = img[li * SN + j];
@@ -826,8 +832,8 @@ __device__ __forceinline__ void c4_durbin(double (&A)[S], double (&B)[S], double
 #pragma unroll
       for (int j = 0; j < S; ++j) img[li * S + j] = A[j];
       wave_lds_sync();
-      // A past k1 is exactly 0; b_m = a_{k1-m} (0 for m > k1: reads down to index -9 land in the guard
-      // or the previous item's image and are dropped by the select)
+      // A past k1 is exactly 0; b_m = a_{k1-m} (0 for m > k1: reads down to index -4 NA - 1 >= -17 land in
+      // the guard or the previous item's image and are dropped by the select)
 #pragma unroll
       for (int j = 0; j < SN; ++j) {
         const int m = li * SN + j;

@@ -41,3 +41,33 @@ def test_dry_run_librispeech_shards_balance_frames():
     assert shards[0][1] == shards[1][0] and shards[1][1] == res["scp_entries"]
     tot = sum(f for _, _, f in shards)
     assert tot <= 600 and all(f >= 0.3 * tot for _, _, f in shards)
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_every_rank_gets_its_pcie_child(gpus):
+    """The PCIe-inclusive pass (with_transfers, SURVEY 8(d) "first H2D to last D2H") runs in a child process
+    of every rank, started before the rank touches the GPU: single-process argv over the rank's own shard,
+    GPU_MAX_HW_QUEUES raised, the rank's GPU only, no rendezvous variables."""
+    res = _run("--gpus", str(gpus), "--utts", "5")
+    ch = res["xfer_children"]
+    assert len(ch) == gpus
+    for r, c in enumerate(ch):
+        a = c["argv"]
+        assert "--xfer-only" in a and "--dry-run" not in a
+        assert a[a.index("--gpus") + 1] == "1" and a.count("--gpus") == 1
+        assert a[a.index("--xfer-shard") + 1] == "%d/%d" % (r, gpus)
+        assert c["env"]["GPU_MAX_HW_QUEUES"] == "8"
+        assert c["env"]["HIP_VISIBLE_DEVICES"] == (str(r) if gpus > 1 else os.environ.get("HIP_VISIBLE_DEVICES"))
+        assert c["rank_env_dropped"] and c["before_gpu_init"]
+
+
+def test_pcie_children_combine():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    got = [{"value": 10.0, "audio_h": 1.0, "elapsed_s": 0.1, "ms_per_step": 10.0, "note": "n"},
+           {"value": 8.0, "audio_h": 1.0, "elapsed_s": 0.125, "ms_per_step": 12.5, "note": "n"}]
+    x = b.combine_xfer_children(got)
+    assert abs(x["value"] - 16.0) < 1e-12 and x["ms_per_step"] == 12.5 and x["per_rank_value"] == [10.0, 8.0]
+    assert b.combine_xfer_children([got[0], None]) is None

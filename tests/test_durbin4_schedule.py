@@ -1,5 +1,5 @@
 """Host-side emulation of durbin4_kernel's data movement (csrc/fdlp_lpc.hip): 4 lanes
-per item, phases S = 1, 3, 5, ... then SL4 = 38 with capacity 4 S and orders k <= 4 S - 2, B updated in place
+per item, phases S = 1, 5, 9, ... then SL4 = 38 with capacity 4 S and orders k <= 4 S - 2, B updated in place
 from its row_shr:1 neighbour (the next item's first lane gets the exact 0 of position 4 S - 1, not a select),
 R1 and A re-laid out through the item's LDS image with B read back mirrored, the 8 positions a phase adds
 loaded one phase ahead.  The emulation keeps the kernel's per-lane slot arrays and checks a and gg against
@@ -10,6 +10,7 @@ import pytest
 from oracle import fdlp_oracle as O
 
 SL4 = 38
+STEP = 4  # kC4Step
 NQ = 4  # quads emulated side by side, so the row_shr:1 crosses item boundaries as on the device
 
 
@@ -32,7 +33,8 @@ def _c4_emulate(r_items, p):
     checks = 0
     while True:
         k1 = min(p, 4 * S - 2)
-        SN = min(S + 2, SL4)
+        SN = min(S + STEP, SL4)
+        NA = SN - S
         while k <= k1:
             acc = part.reshape(nq, 4).sum(1)
             kappa = -acc / E
@@ -56,8 +58,8 @@ def _c4_emulate(r_items, p):
         img = np.zeros((nq, 160))
         for x in range(nl):
             img[qi[x], li[x] * S: li[x] * S + S] = R1[x]
-            for t in range(2):
-                m = 4 * S + 2 * li[x] + t
+            for t in range(NA):
+                m = 4 * S + li[x] + 4 * t
                 img[qi[x], m] = r[qi[x], m + 1] if m <= p else 0.0
         R1 = np.array([img[qi[x], li[x] * SN: li[x] * SN + SN] for x in range(nl)])
         img = np.zeros((nq, 160))
