@@ -145,6 +145,12 @@ int fdlp_compute(fdlp_plan* plan, const fdlp_batch* batch, void* stream);
 /* Keep the fused LPC kernel's a/gg/cep in the workspace (off by default; needed by
  * fdlp_debug_fetch for those three arrays). */
 int fdlp_set_debug(fdlp_plan* plan, int32_t keep_intermediates);
+/* Device range checks (ABI 6): *enabled = 1 in a library built with -DFDLP_DEVICE_CHECKS=1, whose
+ * index-heavy kernels count violated range assertions (descriptors, sample / LDS / exchange indices,
+ * straddle windows, OLA slices) on the device instead of trapping; *violations and *last_line (the
+ * largest failing source line of csrc/) since the last reset; reset != 0 zeroes them.  Synchronises the
+ * current device.  The default build reports enabled = 0 and zeros. */
+int fdlp_device_checks(int32_t* enabled, uint32_t* violations, uint32_t* last_line, int32_t reset);
 /* Autocorrelation algorithm (stage 2).  FDLP_AC_DIRECT: per band, over the taps >= support_eps *
  * peak.  FDLP_AC_STRUCTURED: exact (no tap truncation) skirt-factorised algorithm for the cochlear
  * filterbank with a fixed slope (fbank_type cochlear,..,fixed=1,..; DESIGN.md "Structured

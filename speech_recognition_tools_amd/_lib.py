@@ -131,6 +131,7 @@ SIGNATURES = {
     "fdlp_plan_regions": (c_i32, [c_p, c_p, c_p]),
     "fdlp_plan_flat_events": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_i32]),
     "fdlp_set_lpc_path": (c_i32, [c_p, c_i32]),
+    "fdlp_device_checks": (c_i32, [c_p, c_p, c_p, c_i32]),
     "fdlp_set_dct_path": (c_i32, [c_p, c_i32]),
     "fdlp_dct_path": (c_i32, [c_p]),
     "fdlp_set_pipeline": (c_i32, [c_p, c_i32]),

@@ -407,6 +407,7 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
   const int f = item / c.B, j = item % c.B;
   const int2 reg = c.sk_reg[j];
   const int m1 = reg.x, m2 = reg.y;
+  FDLP_CHECK(0 <= m1 && m1 <= m2 && m2 <= N && j < c.B);
   // the wrap straddle of a band whose first / last nlags - 1 taps are skirt taps is kw Wrap (ac_wrap_kernel)
   const double kw = (VS && rwrap) ? c.sk_wrap[j] : 0.0;
   const double* drow = dct + (int64_t)f * N;
@@ -475,6 +476,7 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
     for (int u = 0; u < kSt; ++u) {  // all loads first: one exposed latency per boundary
       const int pos = b - kWin + 64 * u + lane;
       const int pm = pos < 0 ? 0 : (pos >= N ? pos - N : pos);
+      FDLP_CHECK(pm >= 0 && pm < N);
       wv[u] = wrow[pm];
       dv[u] = drow[pm];
     }
@@ -538,6 +540,7 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
     }
     if (pmask) {
       for (int rest = pmask; rest; rest &= rest - 1) {
+        FDLP_CHECK(__builtin_ctz(rest) < c.fl_H - 1 && fb.x >= 0 && fb.x < kMaxChains);
         const double* po = rpart + (((int64_t)f * (c.fl_H - 1) + __builtin_ctz(rest)) * kMaxChains + fb.x) * nlags;
 #pragma unroll
         for (int g = 0; g < kNB; ++g) fv[g] += po[min(32 * g + (lane >> 1), nlags - 1)];
@@ -745,6 +748,7 @@ __global__ __launch_bounds__(64, vs_waves_per_simd<C>()) void ac_vsweep_kernel(D
       double v = pf[q];
       if constexpr (C == 0) v = pe[q] * v;
       v = (n >= 0 && n < N) ? v : 0.0;
+      FDLP_CHECK(slot >= 0 && slot < kVsRing);
       rg[slot] = v;
       if (slot < kVsMirror) rg[kVsRing + slot] = v;
     }
@@ -795,6 +799,7 @@ __global__ __launch_bounds__(64, vs_waves_per_simd<C>()) void ac_vsweep_kernel(D
       if (i == npend) {
 #pragma unroll
         for (int u = 0; u < A; ++u) pend[i][u] = K * v[u];
+        FDLP_CHECK(band >= 0 && band < B);
         prow[i] = ((int64_t)f * B + band) * nlags;
       }
     }
@@ -860,6 +865,7 @@ __global__ __launch_bounds__(64, vs_waves_per_simd<C>()) void ac_vsweep_kernel(D
   auto block = [&](int n0, double (&lo)[A], const double (&hi)[A]) {
     ensure(n0);
     const int base = slot_add(n0, A * l);
+    FDLP_CHECK(base >= 0 && base + A <= kVsRing + kVsMirror);
 #pragma unroll
     for (int q = 0; q < A; ++q) lo[q] = rg[base + q];
     const double cur = rg[slot_add(n0, l)];
@@ -1014,5 +1020,7 @@ hipError_t launch_autocorr_structured(const DevConsts& c, const double* dct, int
     default: return hipErrorInvalidValue;
   }
 }
+
+hipError_t checks_autocorr(unsigned int* v, bool reset) { return fdlp_checks_local(v, reset); }
 
 }  // namespace fdlp

@@ -29,6 +29,7 @@ __device__ __forceinline__ double makhoul_sample(const DevConsts& c, const Frame
   const int m = c.natural ? n : ((2 * n < N) ? 2 * n : 2 * N - 1 - 2 * n);
   if (dense_rows) return dense_rows[(int64_t)f * N + m];
   const int64_t t = reflect_idx((int64_t)fd.k * c.hop + m - c.ext, fd.T);
+  FDLP_CHECK(dense_rows || (t >= 0 && t < fd.T));
   double s;
   if (pcm_kind == 0) {
     s = (double)((const int16_t*)pcm)[fd.pcm_off + t];
@@ -621,6 +622,7 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
       int u1 = t0 + (4 * q1 < kA * 2 ? 4 * q + 2 : 2 * N - 3 - 4 * q);
       u0 = u0 < 0 ? -u0 : (u0 >= T ? 2 * (T - 1) - u0 : u0);
       u1 = u1 < 0 ? -u1 : (u1 >= T ? 2 * (T - 1) - u1 : u1);
+      FDLP_CHECK(u0 >= 0 && u0 < T && u1 >= 0 && u1 < T);
       pk[2 * q1] = xs[u0];
       pk[2 * q1 + 1] = xs[u1];
     }
@@ -635,6 +637,7 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
   __syncthreads();  // tables
 
   auto frame = [&](const int f) {
+    FDLP_CHECK(f >= 0 && f < nframes);
     const bool fast = !dense_rows && dct1_fast(c, frames[f], pcm_kind);
     // ---- pass 1: thread n2 = C q2 + q3 holds z[BC q1 + n2] (Makhoul order) ----
     double2 y1[kA];
@@ -704,6 +707,7 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
     dct1::pass3_task(t < kAB ? t : 0, k1, k2a, mode);
     double2 y3[kC];
     const int a3 = k2a * kP2 + k1 * kC;
+    FDLP_CHECK(a3 >= 0 && a3 + kC <= kXch && k1 < kA && k2a < kB);
     if (t < kAC) {
 #pragma unroll
       for (int j = 0; j < kB; ++j) xch[j * kP2 + t] = y2[j].x;
@@ -727,6 +731,7 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
     const bool task3 = t < kAB;
     if (task3) rdft<kC>(y3);
     const int lo = k1 + kA * k2a;
+    FDLP_CHECK(lo >= 0 && lo < kAB);
     double2 rl = make_double2(0.0, 0.0), pl = rl;
     if (task3) {
       rl = tab[kRtLo + lo];
@@ -903,5 +908,7 @@ hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const 
   }
   return hipGetLastError();
 }
+
+hipError_t checks_dct(unsigned int* v, bool reset) { return fdlp_checks_local(v, reset); }
 
 }  // namespace fdlp

@@ -117,6 +117,46 @@ __device__ __forceinline__ int xcd_item() {
 static inline int xcd_grid(int total) { return (total + kXcds - 1) / kXcds * kXcds; }
 
 // -----------------------------------------------------------------------------------------
+// Device-side range checks ("HIP bounds-check debug build"): a library built with
+// -DFDLP_DEVICE_CHECKS=1 (python _build.py --out lib/libfdlp_checks.so -DFDLP_DEVICE_CHECKS=1) evaluates
+// FDLP_CHECK(cond) in the index-heavy kernels -- frame descriptors, reflected sample indices, LDS image
+// and exchange indices, straddle windows, OLA slices -- and counts the violations in a per-translation-unit
+// device counter (with the last failing source line) instead of trapping: a trap would end the process in
+// the middle of a batch and leave nothing to read.  fdlp_device_checks() reads (and resets) the counters.
+// In the default build FDLP_CHECK compiles to nothing.
+// -----------------------------------------------------------------------------------------
+#ifndef FDLP_DEVICE_CHECKS
+#define FDLP_DEVICE_CHECKS 0
+#endif
+#if FDLP_DEVICE_CHECKS
+static __device__ unsigned int fdlp_check_state[2];  // violations, largest failing line
+#define FDLP_CHECK(cond)                                                   \
+  do {                                                                     \
+    if (!(cond)) {                                                         \
+      atomicAdd(&fdlp_check_state[0], 1u);                                 \
+      atomicMax(&fdlp_check_state[1], (unsigned int)__LINE__);             \
+    }                                                                      \
+  } while (0)
+// host: this translation unit's counters (violations, line), optionally reset
+static inline hipError_t fdlp_checks_local(unsigned int* v, bool reset) {
+  hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(fdlp_check_state), 2 * sizeof(unsigned int));
+  if (e == hipSuccess && reset) {
+    const unsigned int z[2] = {0u, 0u};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(fdlp_check_state), z, 2 * sizeof(unsigned int));
+  }
+  return e;
+}
+#else
+#define FDLP_CHECK(cond) \
+  do {                   \
+  } while (0)
+static inline hipError_t fdlp_checks_local(unsigned int* v, bool) {
+  v[0] = v[1] = 0u;
+  return hipSuccess;
+}
+#endif
+
+// -----------------------------------------------------------------------------------------
 // wave-level helpers
 // -----------------------------------------------------------------------------------------
 __device__ __forceinline__ double wave_sum(double v) {

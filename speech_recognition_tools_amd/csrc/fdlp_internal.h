@@ -125,6 +125,11 @@ hipError_t launch_dct_frame(const DevConsts& c, const void* pcm, int pcm_kind, c
                             const FrameDesc* frames, const double* dense_rows, int nframes, double* dct,
                             hipStream_t s);
 std::vector<double2> dct_frame_tables(int N, const std::vector<double>& window);
+// FDLP_DEVICE_CHECKS builds: each kernel translation unit's violation counter and last failing line
+hipError_t checks_dct(unsigned int* v, bool reset);
+hipError_t checks_autocorr(unsigned int* v, bool reset);
+hipError_t checks_lpc(unsigned int* v, bool reset);
+hipError_t checks_misc(unsigned int* v, bool reset);
 hipError_t launch_autocorr(const DevConsts& c, const double* dct, const double* dense_rows,
                            int nframes_or_items, double* r, hipStream_t s);
 hipError_t launch_autocorr_structured(const DevConsts& c, const double* dct, int nframes, double* r,

@@ -792,7 +792,9 @@ __host__ __device__ constexpr int c4_item_stride(int SL4) {
   const int need = 4 * SL4;
   return need + ((28 - need % 32) + 32) % 32;
 }
-constexpr int kC4Guard = 24;  // doubles below item 0's image (the mirrored B reads reach index -4 kC4Step - 1)
+constexpr int kC4Guard = 24;
+// the phase that ends at order p holds it: p <= 4 S - 2 = cap - 2
+__device__ __forceinline__ bool k_done_ok(int p, int cap) { return p <= cap - 2; }  // doubles below item 0's image (the mirrored B reads reach index -4 kC4Step - 1)
 
 // Orders [k0, min(p, 4 S - 2)] of phase S, then the next phase.  Returns (in cap) 4 S of the phase that
 // ends at order p and leaves its A in img (positions < cap; exactly 0 past p), gg in g.
@@ -821,6 +823,7 @@ __device__ __forceinline__ void c4_durbin(double (&A)[S], double (&B)[S], double
       // R1 first (B is dead: it is read back mirrored from A's image), then A
       double R1n[SN], An[SN], Bn[SN];
       wave_lds_sync();
+      FDLP_CHECK(4 * SN <= c4_item_stride(SL4) && 4 * S + 4 * NA <= c4_item_stride(SL4));
 #pragma unroll
       for (int j = 0; j < S; ++j) img[li * S + j] = R1[j];
 #pragma unroll
@@ -843,6 +846,7 @@ __device__ __forceinline__ void c4_durbin(double (&A)[S], double (&B)[S], double
 #pragma unroll
       for (int j = 0; j < SN; ++j) {
         const int m = k1 - li * SN - j;
+        FDLP_CHECK(m >= -kC4Guard && m < c4_item_stride(SL4));
         const double v = img[m];
         Bn[j] = m >= 0 ? v : 0.0;
       }
@@ -888,6 +892,7 @@ __global__ __launch_bounds__(64, 2) void durbin4_kernel(const double* __restrict
   double g = 0.0;
   c4_durbin<SL4, 1>(A, B, R1, part, E, rE, img, rrow, p, li, valid, r0, 1, cap, g);
   if (valid && li == 0) gg[item] = g;
+  FDLP_CHECK(cap <= astride && cap <= c4_item_stride(SL4) && (cap & 1) == 0 && k_done_ok(p, cap));
   wave_lds_sync();
   const int half = astride >> 1;
   for (int i = 0; i < 16; ++i) {
@@ -914,13 +919,12 @@ constexpr int kEnvChunk = 5;  // envelope slots held in registers at a time
 // DM: the Durbin phase.  1: the contiguous-chunk Durbin (contig_durbin, p outside durbin8_kernel's
 // range); 2: none, a and gg come from durbin8_kernel (A.a_ext, A.gg_ext; default where it is instantiated).
 constexpr int kDmContig = 1, kDmExt = 2;
-#ifndef FDLP_LAT_WAVES
-#define FDLP_LAT_WAVES 4  // waves per SIMD the lattice kernel is compiled for (register budget)
-#endif
-// the super-block cepstrum (CB < 0) holds ~70 doubles of window, H rows and accumulators (spills at 3
-// waves per SIMD); its LDS allows 2.5 per SIMD anyway
+// waves per SIMD the lattice kernel is compiled for (register budget).  CB > 0: 4 (127 VGPRs and 12 spilled
+// once per group: 0.62 ms per 327 680 items against 0.68 at 3 waves without spills, r04d); the super-block
+// cepstrum (CB < 0) holds ~70 doubles of window, H rows and accumulators (spills at 3 waves per SIMD); its
+// LDS allows 2.5 per SIMD anyway
 template <int CB>
-constexpr int lat_waves() { return CB < 0 ? 2 : FDLP_LAT_WAVES; }
+constexpr int lat_waves() { return CB < 0 ? 2 : 4; }
 template <int SL, int CB = 0, int DM = kDmContig>
 __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(LpcEnvArgs A_) {
   extern __shared__ double sh[];
@@ -941,6 +945,7 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
 #pragma unroll
       for (int g2 = 0; g2 < 4; ++g2) {
         const int it = min(grp * 4 + g2, A.items - 1);
+        FDLP_CHECK(it >= 0 && A.la_len <= A.a_stride && A.la_len <= A.region);
         const double* src = A.a_ext + (int64_t)it * A.a_stride;  // la_len doubles, 16-B aligned rows
         double* dst = sh + g2 * A.region;
         for (int c0 = 0; c0 < A.la_len; c0 += 128) {  // 64 lanes x 16 B = 128 doubles per copy
@@ -1008,13 +1013,24 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
     wave_lds_sync();
     // ---- phase 2: cepstrum (features.py:233-246), as in lpc_env_kernel -------------------------
     if constexpr (CB > 0) {
-      double kc[CB];  // lane l: n c_n for n = 16 b + l of every finished block b (0 for n = 0)
+      // d_n = n c_n = y_n - sum_{k in the block, k < n} d_k a_{n-k}, y_n = -n a_n - (finished blocks' terms):
+      // a unit lower-triangular Toeplitz system per block, solved by the first 16 terms of the impulse
+      // response of 1/a(z) (h_0 = 1, h_m = -sum a_k h_{m-k}, once per item): d = H y, 16 broadcast FMAs in 4
+      // chains instead of a 16-step serial recurrence (the form the REVERB super-blocks use, features.py:243-245)
+      double kc[CB];  // lane l: d_n = n c_n for n = 16 b + l of every finished block b (0 for n = 0)
+      double Hrow[16];
+      {
+        double t = l >= 1 ? la[l] : 0.0;  // sum_{i < l} h_i a_{l-i}, so far i = 0
+        double hl = l == 0 ? 1.0 : 0.0;
+        sb_impulse<1>(hl, t, la, l);
+        Hrow[0] = hl;
+        sb_hrow<1>(Hrow, hl);
+      }
 #pragma unroll
       for (int b = 0; b < CB; ++b) {
         const int b0 = 16 * b;
         if (b0 >= ((FDLP_LPC_PHASES & 2) ? M : 0)) break;
         const int n = b0 + l;
-        const double inv_n = 1.0 / (double)(n > 0 ? n : 1);
         double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
         if (b > 0) asm volatile("s_nop 1");  // kc[b - 1] was just written: DPP reads need 2 wait states
 #pragma unroll
@@ -1022,10 +1038,11 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
           const double* al = la + n - 16 * bp;  // alpha_{n - k} = la[n - k], k = 16 bp + j
           cep_terms16(a0, a1, a2, a3, kc[bp], al);
         }
-        double acc = (a0 + a1) + (a2 + a3);
-        double mine = 0.0;
-        cep_block_step<0>(b0, M, l, gg, inv_n, la, n, acc, mine, p);
-        kc[b] = n == 0 ? 0.0 : (double)n * mine;
+        const double an = n <= p ? la[min(n, p)] : 0.0;
+        const double y = -(double)n * an - ((a0 + a1) + (a2 + a3));
+        const double d = sb_solve(y, Hrow);
+        const double mine = n == 0 ? log(sqrt(gg)) : d * (1.0 / (double)(n > 0 ? n : 1));
+        kc[b] = d;  // 0 for n = 0 (y_0 = 0)
         if (n < CSN) cs[n] = mine;
         if (n < M && valid && A.cep_out) A.cep_out[(int64_t)item * M + n] = mine;
       }
@@ -1494,5 +1511,7 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
     default: return hipErrorInvalidValue;
   }
 }
+
+hipError_t checks_lpc(unsigned int* v, bool reset) { return fdlp_checks_local(v, reset); }
 
 }  // namespace fdlp

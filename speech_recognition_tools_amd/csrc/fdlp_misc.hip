@@ -49,6 +49,7 @@ __global__ __launch_bounds__(256) void ola_log_tiled_kernel(DevConsts c, const d
     const FrameDesc fd = frames[U.frame0 + k];
     const int t = t0 + tt;
     if (t < t0 + nt && t >= fd.dst && t < fd.dst + fd.cnt) {
+      FDLP_CHECK(fd.src + (t - fd.dst) >= 0 && fd.src + (t - fd.dst) < kk && k < U.F && t < U.L);
       const double* er = env + (int64_t)(U.frame0 + k) * B * kk + fd.src + (t - fd.dst);
       for (int j = jj; j < B; j += blockDim.x / kOlaRows) tile[tt * BS + j] = tile[tt * BS + j] + er[(int64_t)j * kk];
     }
@@ -596,5 +597,7 @@ hipError_t launch_modspec_out(const double* cep, const FrameDesc* frames, const 
   return hipGetLastError();
 }
 
+
+hipError_t checks_misc(unsigned int* v, bool reset) { return fdlp_checks_local(v, reset); }
 
 }  // namespace fdlp

@@ -1,5 +1,8 @@
 // fdlp_plan.cpp -- plan (setup of getFeats, computeFDLPSpectrogram.py:43-118), batch geometry,
 // OLA tables and the kernel pipeline behind fdlp_compute (getFeats :159-229).
+#ifndef FDLP_DEVICE_CHECKS
+#define FDLP_DEVICE_CHECKS 0
+#endif
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -1146,6 +1149,23 @@ int fdlp_set_debug(fdlp_plan* p, int32_t keep_intermediates) {
     if (!p->ws.cep) HIP_TRY(hipMalloc((void**)&p->ws.cep, sizeof(double) * items * p->M));
   }
   p->debug_intermediates = keep_intermediates != 0;
+  return FDLP_OK;
+}
+
+int fdlp_device_checks(int32_t* enabled, uint32_t* violations, uint32_t* last_line, int32_t reset) {
+  unsigned int tot = 0, line = 0;
+  hipError_t (*const fns[])(unsigned int*, bool) = {fdlp::checks_dct, fdlp::checks_autocorr, fdlp::checks_lpc,
+                                                    fdlp::checks_misc};
+  HIP_TRY(hipDeviceSynchronize());
+  for (auto fn : fns) {
+    unsigned int v[2] = {0u, 0u};
+    HIP_TRY(fn(v, reset != 0));
+    tot += v[0];
+    line = std::max(line, v[1]);
+  }
+  if (enabled) *enabled = FDLP_DEVICE_CHECKS ? 1 : 0;
+  if (violations) *violations = tot;
+  if (last_line) *last_line = line;
   return FDLP_OK;
 }
 

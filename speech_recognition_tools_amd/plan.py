@@ -267,3 +267,11 @@ class FdlpPlan:
         check(lib.fdlp_cepstrum_rows(self._h, a.data_ptr(), gg.data_ptr(), n, p1 - 1, int(lim), cep.data_ptr(),
                                      s.cuda_stream))
         return cep
+
+
+def device_checks(reset: bool = False):
+    """(enabled, violations, last_line) of the device range checks (fdlp_device_checks): enabled only in a
+    library built with -DFDLP_DEVICE_CHECKS=1 (loaded through FDLP_LIB); synchronises the device."""
+    en, v, ln = ctypes.c_int32(), ctypes.c_uint32(), ctypes.c_uint32()
+    check(lib.fdlp_device_checks(ctypes.byref(en), ctypes.byref(v), ctypes.byref(ln), int(bool(reset))))
+    return bool(en.value), int(v.value), int(ln.value)
