@@ -428,6 +428,18 @@ def run_xfer_child(args, world=1, rank=0, local=0):
     return json.loads(lines[-1])["with_transfers"]
 
 
+def host_cores():
+    """The host cores this process may use: its CPU affinity, capped at the CPU share a pool gives a job
+    (OMP_NUM_THREADS, which the GPU pool sets to a one-GPU job's share; os.cpu_count() there counts every
+    CPU of the machine, most of them other jobs')."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(share))) if share.isdigit() and int(share) > 0 else max(1, n)
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -437,7 +449,8 @@ def parse_args(argv=None):
     ap.add_argument("--utts", type=int, default=1024, help="utterances per step per GPU (wsj workload)")
     ap.add_argument("--seconds", type=float, default=4.0, help="utterance length (wsj workload)")
     ap.add_argument("--support-eps", type=float, default=None)
-    ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cpu-workers", type=int, default=host_cores(),
+                    help="CPU-baseline processes (default: every host core this process may use)")
     ap.add_argument("--cpu-per-worker", type=int, default=None,
                     help="utterances per CPU-baseline process (default: about 10 s of oracle time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
