@@ -9,7 +9,11 @@
 # (e2e/wsj/run_fdlp_e1.sh:196), spreads its JOBs over the node), --jobs_per_gpu K (without $cmd: at most
 # N*K JOBs run at once; default 2), --job_mem / --job_gpu (the resource request a $cmd launcher gets for
 # every JOB: "$cmd --mem 5G --gpu 1 JOB=1:$nj ...", the reference's --mem 5G (:92, :141) plus one GPU, so
-# queue.pl / slurm.pl allocate the MI355X the JOB runs on; run.pl ignores both; --job_gpu 0 drops it).
+# queue.pl / slurm.pl allocate the MI355X the JOB runs on; run.pl ignores both; --job_gpu 0 drops it),
+# --resume true (per-JOB resume: every JOB that finishes leaves <feat_dir>/melspec_<name>.JOB.done holding
+# a hash of its shard and the feature options; a rerun with --resume true skips the JOBs whose stamp
+# matches and whose ark/scp exist, through scripts/fdlp_resume_guard.sh, and reruns the rest; the
+# concatenated feats.scp / utt2num_frames are rebuilt from every JOB's files as usual).
 #
 #   make_FDLPspectrum_feats.sh [--opts] <data_dir> <feat_dir>
 # Inputs: <data_dir>/wav.scp or <data_dir>/segments.  Outputs: <data_dir>/feats.scp,
@@ -44,6 +48,7 @@ seed=
 noise_seed=
 job_mem=5G     # $cmd --mem (the reference driver's request, make_FDLPspectrum_feats.sh:92, :141)
 job_gpu=1      # $cmd --gpu (0: no GPU request)
+resume=false   # skip JOBs whose last finished run had the same shard and options (and whose outputs exist)
 
 if [ -f utils/parse_options.sh ]; then
   . utils/parse_options.sh || exit 1
@@ -107,36 +112,65 @@ split_list() {  # split_list <in> <out1> ... : contiguous, balanced, like utils/
   python3 "$here/speech_recognition_tools_amd/shard.py" "$in" "$@"
 }
 
+feat_opts="--fbank_type=$fbank_type --gamma_weight=$gamma_weight --add_reverb=$add_reverb \
+--add_noise=$add_noise --coeff_num=$coeff_num --coeff_range=$coeff_range --order=$order \
+--overlap_fraction=$overlap_fraction --nfilters=$nfilters --fduration=$fduration --frate=$frate"
+
+job_key() {  # job_key <n> <shard> <scp-type-opt>: the JOB's identity, written to its key file
+  local n=$1 shard=$2 stype=$3
+  { echo "$add_opts $stype $feat_opts compute_cmvn=$compute_cmvn"; cat "$shard"; } | cksum > "$log_dir/resume_${name}.$n.key"
+}
+job_done() {  # the JOB's last finished run had the same key and its outputs exist
+  local n=$1 out="$feat_dir/melspec_${name}.$1"
+  cmp -s "$log_dir/resume_${name}.$n.key" "$out.done" && [ -f "$out.ark" ] && [ -f "$out.scp" ]
+}
+
 run_jobs() {  # run_jobs <list-pattern containing JOB> <scp-type-opt>
   local pattern=$1 stype=$2
-  local cmvn_opt=
+  local cmvn_opt= n pending=()
   $compute_cmvn && cmvn_opt="--cmvn_stats $feat_dir/cmvn_${name}.JOB.mat"
-  if [ -n "$cmd" ]; then
-    local req=
-    [ -n "$job_mem" ] && req="--mem $job_mem"
-    [ "${job_gpu:-0}" != 0 ] && req="$req --gpu $job_gpu"
-    $cmd $req JOB=1:$nj "$log_dir/feats_${name}.JOB.log" \
-      python3 "$cli" "$pattern" "$feat_dir/melspec_${name}.JOB" $add_opts $cmvn_opt $stype --device_rr=JOB,$ngpu \
-        --fbank_type=$fbank_type --gamma_weight=$gamma_weight --add_reverb=$add_reverb \
-        --add_noise=$add_noise --coeff_num=$coeff_num --coeff_range=$coeff_range --order=$order \
-        --overlap_fraction=$overlap_fraction --nfilters=$nfilters --fduration=$fduration \
-        --frate=$frate || exit 1
-    return 0
-  fi
-  local pids=() n fail=0
   for n in $(seq $nj); do
-    python3 "$cli" "${pattern//JOB/$n}" "$feat_dir/melspec_${name}.$n" $add_opts ${cmvn_opt//JOB/$n} $stype --device_rr=$n,$ngpu \
-      --fbank_type=$fbank_type --gamma_weight=$gamma_weight --add_reverb=$add_reverb \
-      --add_noise=$add_noise --coeff_num=$coeff_num --coeff_range=$coeff_range --order=$order \
-      --overlap_fraction=$overlap_fraction --nfilters=$nfilters --fduration=$fduration \
-      --frate=$frate > "$log_dir/feats_${name}.$n.log" 2>&1 &
-    pids+=($!)
-    if [ ${#pids[@]} -ge $(( ngpu * jobs_per_gpu )) ]; then
-      wait "${pids[0]}" || fail=1
-      pids=("${pids[@]:1}")
+    job_key $n "${pattern//JOB/$n}" "$stype"
+    if $resume && job_done $n; then
+      echo "$0: JOB $n is up to date (--resume true), skipped"
+    else
+      rm -f "$feat_dir/melspec_${name}.$n.done"
+      pending+=($n)
     fi
   done
-  for p in "${pids[@]}"; do wait "$p" || fail=1; done
+  [ ${#pending[@]} -eq 0 ] && return 0
+  if [ -n "$cmd" ]; then
+    local req= guard=()
+    [ -n "$job_mem" ] && req="--mem $job_mem"
+    [ "${job_gpu:-0}" != 0 ] && req="$req --gpu $job_gpu"
+    # with --resume the launcher still gets the whole JOB array (JOB=a:b is a range); the guard skips
+    # the finished JOBs inside it
+    $resume && guard=(bash "$here/scripts/fdlp_resume_guard.sh" "$log_dir/resume_${name}.JOB.key"
+                      "$feat_dir/melspec_${name}.JOB.done" "$feat_dir/melspec_${name}.JOB" --)
+    $cmd $req JOB=1:$nj "$log_dir/feats_${name}.JOB.log" \
+      "${guard[@]}" python3 "$cli" "$pattern" "$feat_dir/melspec_${name}.JOB" $add_opts $cmvn_opt $stype \
+        --device_rr=JOB,$ngpu $feat_opts || exit 1
+    $resume || for n in $(seq $nj); do cp "$log_dir/resume_${name}.$n.key" "$feat_dir/melspec_${name}.$n.done"; done
+    return 0
+  fi
+  local pids=() jobs=() fail=0
+  for n in "${pending[@]}"; do
+    python3 "$cli" "${pattern//JOB/$n}" "$feat_dir/melspec_${name}.$n" $add_opts ${cmvn_opt//JOB/$n} $stype \
+      --device_rr=$n,$ngpu $feat_opts > "$log_dir/feats_${name}.$n.log" 2>&1 &
+    pids+=($!)
+    jobs+=($n)
+    if [ ${#pids[@]} -ge $(( ngpu * jobs_per_gpu )) ]; then
+      if wait "${pids[0]}"; then cp "$log_dir/resume_${name}.${jobs[0]}.key" "$feat_dir/melspec_${name}.${jobs[0]}.done"
+      else fail=1; fi
+      pids=("${pids[@]:1}")
+      jobs=("${jobs[@]:1}")
+    fi
+  done
+  local i
+  for i in "${!pids[@]}"; do
+    if wait "${pids[$i]}"; then cp "$log_dir/resume_${name}.${jobs[$i]}.key" "$feat_dir/melspec_${name}.${jobs[$i]}.done"
+    else fail=1; fi
+  done
   [ $fail -eq 0 ] || { echo "$0: a JOB failed, see $log_dir/feats_${name}.*.log"; exit 1; }
 }
 

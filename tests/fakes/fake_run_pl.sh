@@ -13,5 +13,7 @@ for n in $(seq "${range%%:*}" "${range##*:}"); do
   args=()
   for a in "$@"; do args+=("${a//JOB/$n}"); done
   printf '%s\n' "${args[*]}" >> "$FAKE_CMD_LOG"
-  touch "${args[3]}.scp" "${args[3]}.len"
+  for i in "${!args[@]}"; do  # the output prefix follows "<cli>.py <list>"
+    [[ "${args[$i]}" == *.py ]] && { touch "${args[$((i + 2))]}.scp" "${args[$((i + 2))]}.len"; break; }
+  done
 done

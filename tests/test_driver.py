@@ -135,3 +135,99 @@ def test_native_jobs_open_only_their_gpu(monkeypatch):
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "4,5,6,7")
     a = narrow_visible_devices(build_parser().parse_args(["a.scp", "o", "--device_rr=2,4"]), env)
     assert env["HIP_VISIBLE_DEVICES"] == "5" and a.device == 0
+
+
+FAKE_CLI = r'''
+import os, sys
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+lst, out = args[0], args[1]
+with open(os.environ["FAKE_CLI_LOG"], "a") as f:
+    f.write(out + "\n")
+utts = [l.split()[0] for l in open(lst) if l.strip()]
+open(out + ".ark", "w").write("ark")
+open(out + ".scp", "w").write("".join("%s %s.ark:%d\n" % (u, out, i) for i, u in enumerate(utts)))
+open(out + ".len", "w").write("".join("%s 1\n" % u for u in utts))
+'''
+
+
+def _resume_setup(tmp_path):
+    src = tmp_path / "src" / "featgen"
+    src.mkdir(parents=True)
+    (src / "computeFDLPSpectrogram.py").write_text(FAKE_CLI)
+    data = tmp_path / "data" / "dev"
+    data.mkdir(parents=True)
+    (data / "wav.scp").write_text("".join("u%d /x/u%d.wav\n" % (i, i) for i in range(9)))
+    log = tmp_path / "cli.log"
+
+    def run(*extra):
+        if log.exists():
+            log.unlink()
+        cmd = ["bash", os.path.join(ROOT, "scripts", "make_FDLPspectrum_feats.sh"), "--nj", "3", "--ngpu", "1",
+               "--src_dir", str(tmp_path / "src"), "--write_utt2num_frames", "true"] + list(extra) + [
+               str(data), str(tmp_path / "fbank")]
+        r = subprocess.run(cmd, cwd=str(tmp_path), env=dict(os.environ, FAKE_CLI_LOG=str(log)),
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        ran = sorted(int(l.rsplit(".", 1)[1]) for l in log.read_text().split()) if log.exists() else []
+        assert len((data / "feats.scp").read_text().splitlines()) == 9
+        assert len((data / "utt2num_frames").read_text().splitlines()) == 9
+        return ran
+    return run, tmp_path / "fbank"
+
+
+def test_driver_resume_skips_finished_jobs(tmp_path):
+    """--resume true (SURVEY.md §5 checkpoint/resume row): a rerun skips the JOBs whose last finished run
+    had the same shard and options and whose ark/scp exist; a JOB whose output went missing, or a change of
+    the feature options, reruns; without --resume every JOB runs as in the reference driver."""
+    run, fbank = _resume_setup(tmp_path)
+    assert run() == [1, 2, 3]
+    assert all((fbank / ("melspec_dev.%d.done" % n)).exists() for n in (1, 2, 3))
+    assert run("--resume", "true") == []
+    (fbank / "melspec_dev.2.ark").unlink()
+    assert run("--resume", "true") == [2]
+    assert run("--resume", "true", "--order", "40") == [1, 2, 3]  # other options: new keys
+    assert run("--resume", "true", "--order", "40") == []
+    assert run() == [1, 2, 3]
+
+
+def test_driver_resume_with_launcher_wraps_jobs_in_the_guard(tmp_path):
+    """With a $cmd launcher the JOB array is still launched whole (JOB=1:n is a range) and every JOB runs
+    behind scripts/fdlp_resume_guard.sh; the command after the guard's "--" is the unguarded JOB argv."""
+    data = tmp_path / "data" / "dev"
+    data.mkdir(parents=True)
+    (data / "wav.scp").write_text("".join("u%d /x/u%d.wav\n" % (i, i) for i in range(4)))
+    logs = []
+    for extra in ([], ["--resume", "true"]):
+        log = tmp_path / ("cmd%d.log" % len(logs))
+        env = dict(os.environ, FAKE_CMD_LOG=str(log), HIP_VISIBLE_DEVICES="0,1")
+        cmd = ["bash", os.path.join(ROOT, "scripts", "make_FDLPspectrum_feats.sh"), "--nj", "2"] + extra + [
+               "--cmd", os.path.join(ROOT, "tests", "fakes", "fake_run_pl.sh"), str(data), str(tmp_path / "fbank")]
+        r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        logs.append(log.read_text().splitlines())
+    for plain, guarded in zip(*logs):
+        g = guarded.split()
+        assert g[0] == "bash" and g[1].endswith("fdlp_resume_guard.sh")
+        assert " ".join(g[g.index("--") + 1:]) == plain
+
+
+def test_resume_guard(tmp_path):
+    guard = os.path.join(ROOT, "scripts", "fdlp_resume_guard.sh")
+    key, stamp, out = tmp_path / "k", tmp_path / "s", tmp_path / "o"
+    key.write_text("1 2\n")
+    mark = tmp_path / "ran"
+
+    def go(*command):
+        if mark.exists():
+            mark.unlink()
+        r = subprocess.run(["bash", guard, str(key), str(stamp), str(out), "--"] + list(command),
+                           capture_output=True, text=True, timeout=60)
+        return r.returncode, mark.exists()
+    assert go("false") == (1, False) and not stamp.exists()  # a failed JOB leaves no stamp
+    assert go("touch", str(mark)) == (0, True) and stamp.read_text() == "1 2\n"
+    assert go("touch", str(mark)) == (0, True)  # stamp matches but no outputs yet: runs
+    (tmp_path / "o.ark").write_text("")
+    (tmp_path / "o.scp").write_text("")
+    assert go("touch", str(mark)) == (0, False)  # up to date: skipped
+    key.write_text("3 4\n")
+    assert go("touch", str(mark)) == (0, True) and stamp.read_text() == "3 4\n"
