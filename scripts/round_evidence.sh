@@ -21,6 +21,8 @@ for pmc in FETCH_SIZE WRITE_SIZE "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES" "SQ_
 done
 python3 scripts/pmc_report.py "$O/pmc_*/*.db" $O/pmc.json > $O/pmc.txt 2>&1 || true
 cp $O/pmc.json profiles/${TAG}_pmc.json
+# the raw databases stay on the box (gpurun copies back at most 64 MiB of gpurun_out/); KEEP_DB=1 keeps them
+[ -z "${KEEP_DB:-}" ] && rm -rf $O/trace $O/pmc_*/
 [ -n "${SKIP_BENCH:-}" ] && exit 0
 timeout -k 10 600 python3 bench.py > $O/bench_full.log 2>&1 || { echo "bench failed"; tail -20 $O/bench_full.log; exit 2; }
 tail -1 $O/bench_full.log
