@@ -577,13 +577,12 @@ __device__ __forceinline__ void pass3_task(int t, int& k1, int& k2a, int& mode) 
 }
 }  // namespace dct1
 
-// Frames of the fast gather: int16 PCM without noise or the diff filter whose reflect padding
+// Frames of the fast gather: int16 PCM (noise-mixed or not; not the diff filter) whose reflect padding
 // (numpy 'reflect', features.py:146) is at most one bounce, sample u -> -u below 0 and 2(T-1) - u from T on
 // (every frame of an utterance longer than the half window; the others take the general gather).
 __device__ __forceinline__ bool dct1_fast(const DevConsts& c, const FrameDesc& fd, int pcm_kind) {
   const int64_t t0 = (int64_t)fd.k * c.hop - c.ext;
-  return pcm_kind == 0 && fd.noise_off < 0 && fd.T >= 2 && t0 >= -(fd.T - 1) &&
-         t0 + 2 * dct1::kM - 1 <= 2 * (fd.T - 1);
+  return pcm_kind == 0 && fd.T >= 2 && t0 >= -(fd.T - 1) && t0 + 2 * dct1::kM - 1 <= 2 * (fd.T - 1);
 }
 
 // Two frames per workgroup (f = 2 b, 2 b + 1), as straight-line code: the tables are staged once per two
@@ -631,6 +630,39 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
 #pragma unroll
     for (int q1 = 0; q1 < kA; ++q1) wv[q1] = hwin[kBC * q1 + t];
   };
+  // noise-mixed frames (features.py:31, sig + alp * ns in fp64 without contraction, as makhoul_sample):
+  // y1 holds the window; the samples and the noise at the same reflected positions arrive in two halves
+  // (80 int registers for all of them at once would not fit next to y1)
+  auto load_mixed = [&](double2 (&y)[kA], const FrameDesc& fd) {
+    const int16_t* xs = (const int16_t*)pcm + fd.pcm_off;
+    const int16_t* ns = noise + fd.noise_off;
+    const int t0 = (int)((int64_t)fd.k * c.hop - c.ext), T = fd.T;
+    constexpr int kHalf = kA / 2;
+#pragma unroll
+    for (int h = 0; h < kA; h += kHalf) {
+      int px[2 * kHalf], pn[2 * kHalf];
+#pragma unroll
+      for (int q1 = h; q1 < h + kHalf; ++q1) {
+        const int q = kBC * q1 + t;
+        int u0 = t0 + (4 * q1 < kA * 2 ? 4 * q : 2 * N - 1 - 4 * q);
+        int u1 = t0 + (4 * q1 < kA * 2 ? 4 * q + 2 : 2 * N - 3 - 4 * q);
+        u0 = u0 < 0 ? -u0 : (u0 >= T ? 2 * (T - 1) - u0 : u0);
+        u1 = u1 < 0 ? -u1 : (u1 >= T ? 2 * (T - 1) - u1 : u1);
+        FDLP_CHECK(u0 >= 0 && u0 < T && u1 >= 0 && u1 < T);
+        px[2 * (q1 - h)] = xs[u0];
+        px[2 * (q1 - h) + 1] = xs[u1];
+        pn[2 * (q1 - h)] = ns[u0];
+        pn[2 * (q1 - h) + 1] = ns[u1];
+      }
+#pragma unroll
+      for (int q1 = h; q1 < h + kHalf; ++q1) {
+        const double s0 = __dadd_rn((double)px[2 * (q1 - h)], __dmul_rn(fd.alpha, (double)pn[2 * (q1 - h)]));
+        const double s1 = __dadd_rn((double)px[2 * (q1 - h) + 1], __dmul_rn(fd.alpha, (double)pn[2 * (q1 - h) + 1]));
+        y[q1].x = __dmul_rn(s0, y[q1].x);
+        y[q1].y = __dmul_rn(s1, y[q1].y);
+      }
+    }
+  };
 
   const int f0 = kDctFramesPerBlock * (int)blockIdx.x;
   for (int q = t; q < kTabs; q += kThreads) tab[q] = c.dct1_tw[q];
@@ -643,17 +675,23 @@ __global__ __launch_bounds__(dct1::kThreads) void dct_frame_kernel(DevConsts c, 
     double2 y1[kA];
     if (fast) {
       if (t < kBC) {
-        int pk[2 * kA];
-        load_samples(pk, f);
-        load_window(y1);
+        const FrameDesc fd = frames[f];
+        if (fd.noise_off < 0) {
+          int pk[2 * kA];
+          load_samples(pk, f);
+          load_window(y1);
 #pragma unroll
-        for (int q1 = 0; q1 < kA; ++q1) {
-          y1[q1].x = __dmul_rn((double)pk[2 * q1], y1[q1].x);
-          y1[q1].y = __dmul_rn((double)pk[2 * q1 + 1], y1[q1].y);
+          for (int q1 = 0; q1 < kA; ++q1) {
+            y1[q1].x = __dmul_rn((double)pk[2 * q1], y1[q1].x);
+            y1[q1].y = __dmul_rn((double)pk[2 * q1 + 1], y1[q1].y);
+          }
+        } else {
+          load_window(y1);
+          load_mixed(y1, fd);
         }
       }
     } else {
-      // general frames (multi-bounce reflect padding, noise mixing, the diff filter, fp64 input, dense rows):
+      // general frames (multi-bounce reflect padding, the diff filter, fp64 input, dense rows):
       // the samples are staged through xch by a rolled loop (the general gather is too large to unroll 40x),
       // real parts then imaginary parts; the branch is uniform over the workgroup
       FrameDesc fd;
