@@ -573,7 +573,9 @@ __device__ __forceinline__ void contig_durbin(double (&A)[S], double (&B)[S], do
 // (features.py:226-228); only the summation order of the order-k dot product differs (8 lane partials).
 // -----------------------------------------------------------------------------------------
 constexpr int kD8Chains = 4;  // the next order's dot product in 4 chains (2: no difference, 1.13 vs 1.14 ms)
-constexpr int kNewton = 2;    // Newton steps after v_rcp_f64 for 1/E (one: parity green, time within noise)
+constexpr int kNewton = 1;    // Newton steps after v_rcp_f64 for 1/E: one (durbin4_kernel 0.693-0.711 ->
+                              // 0.680-0.696 ms alternating, profiles/r04m_newton_ab.txt; per-item a within
+                              // durbin8's accuracy against solve_toeplitz, test_durbin4_matches_durbin8)
 template <int S>
 __device__ __forceinline__ void c8_step(double (&A)[S], const double (&Bs)[S], double (&Bd)[S],
                                         const double (&R1)[S], double& part, double& E, bool first) {
