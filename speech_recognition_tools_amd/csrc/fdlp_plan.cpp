@@ -160,15 +160,33 @@ struct SkirtTables {
   bool wrap_any = false;
 };
 
-// Split the flat sweep [fl_lo, fl_hi) into H equal position parts (more waves: the flat sweep has one
-// unit per frame against two for the skirts).  Part h covers [P_{h+1}, P_h) and takes the events with
-// P_{h+1} <= S < P_h (part 0 also S = fl_hi).  Band j needs the partial chain of part h when its flat top
-// crosses the part's lower end: m1_j < P_{h+1} < m2_j.
+// Split the flat sweep [fl_lo, fl_hi) into H parts of equal work (more waves: the flat sweep has one unit
+// per frame against two for the skirts): a position costs 1, an event (restart or emission: the fold into
+// every chain, the masked extra pass of the block it splits) kFlatEventCost positions -- fitted to the
+// recipes' sweep (A = 10 lags per lane, C = 5 chains) from per-wave timings, where equal position parts
+// ran 858 / 1067 us (median) with 34 / 126 events.  Part h covers [P_{h+1}, P_h) and takes
+// the events with P_{h+1} <= S < P_h (part 0 also S = fl_hi).  Band j needs the partial chain of part h
+// when its flat top crosses the part's lower end: m1_j < P_{h+1} < m2_j.
+constexpr double kFlatEventCost = 35.0;
 void flat_parts(SkirtTables* T, int B, int H) {
   if (T->fl_hi - T->fl_lo < 1024 * H) H = 1;
   T->fl_H = H;
   std::vector<int> P(H + 1);
-  for (int h = 0; h <= H; ++h) P[h] = T->fl_hi - (int)((int64_t)(T->fl_hi - T->fl_lo) * h / H);
+  {
+    // cost above position n (sweep order: top down), then the cut points at h / H of the total
+    const int lo = T->fl_lo, hi = T->fl_hi, len = hi - lo;
+    std::vector<double> above(len + 1, 0.0);  // above[i]: cost of positions [hi - i, hi) and their events
+    std::vector<int> ev_at(len + 1, 0);
+    for (const auto& e : T->fl) ev_at[std::min(std::max(hi - e.S, 0), len)] += 1;
+    for (int i = 1; i <= len; ++i) above[i] = above[i - 1] + 1.0 + kFlatEventCost * ev_at[i];
+    P[0] = hi;
+    P[H] = lo;
+    for (int h = 1, i = 0; h < H; ++h) {
+      const double target = above[len] * h / H;
+      while (i < len && above[i] < target) ++i;
+      P[h] = hi - i;
+    }
+  }
   for (int h = 0; h < H; ++h) { T->part_hi[h] = P[h]; T->part_lo[h] = P[h + 1]; }
   const int nev = (int)T->fl.size();
   T->part_ev[0] = 0;
