@@ -1136,13 +1136,29 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
     const double* mask = A.weights;
     const double* lif = A.weights + M;
     const double* gam = A.weights + 2 * M;
-    for (int n = l; n < A.Me; n += 16) {
-      double v = cs[n];
-      v = v * mask[n];
-      v = v * lif[n];
-      v = v * gam[n];
-      if (A.odd_zero && (n & 1)) v = 0.0;
-      cw[n] = v;
+    // four coefficients per lane at a time: their 12 weight loads issue together (one exposed latency per
+    // four, not per coefficient), the products in the reference's order
+    for (int n0 = l; n0 < A.Me; n0 += 64) {
+      double wm[4], wl[4], wg[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int n = min(n0 + 16 * k, A.Me - 1);  // clamped: the loads are unconditional
+        wm[k] = mask[n];
+        wl[k] = lif[n];
+        wg[k] = gam[n];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int n = n0 + 16 * k;
+        if (n < A.Me) {
+          double v = cs[n];
+          v = v * wm[k];
+          v = v * wl[k];
+          v = v * wg[k];
+          if (A.odd_zero && (n & 1)) v = 0.0;
+          cw[n] = v;
+        }
+      }
     }
     wave_lds_sync();
     if constexpr (CB < 0) {
