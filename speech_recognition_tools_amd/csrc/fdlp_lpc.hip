@@ -836,21 +836,21 @@ __device__ __forceinline__ void c4_durbin(double (&A)[S], double (&B)[S], double
       wave_lds_sync();
 #pragma unroll
       for (int j = 0; j < S; ++j) img[li * S + j] = A[j];
+#pragma unroll
+      for (int t = 0; t < NA; ++t) img[4 * S + li + 4 * t] = 0.0;  // the staged R1 positions back to 0
       wave_lds_sync();
-      // A past k1 is exactly 0; b_m = a_{k1-m} (0 for m > k1: reads down to index -4 NA - 1 >= -17 land in
-      // the guard or the previous item's image and are dropped by the select)
+      // No selects: A past k1 = 4 S - 2 is exactly +0 in the image, [4 S, 4 SN) was just zeroed and
+      // [4 SN, kItem) of every item is still the 0 of the kernel's first pass, so the An reads (< 4 SN) and
+      // the mirrored Bn reads (b_m = a_{k1-m}, down to index -4 NA - 1, into the guard or the previous item's
+      // [kItem - 4 NA - 1, kItem) c [4 SN, kItem)) see exact zeros wherever the recursion needs them.
+      constexpr int k1c = 4 * S - 2;
+      FDLP_CHECK(k1 == k1c);
+#pragma unroll
+      for (int j = 0; j < SN; ++j) An[j] = img[li * SN + j];
 #pragma unroll
       for (int j = 0; j < SN; ++j) {
-        const int m = li * SN + j;
-        const double v = img[m];
-        An[j] = m <= k1 ? v : 0.0;
-      }
-#pragma unroll
-      for (int j = 0; j < SN; ++j) {
-        const int m = k1 - li * SN - j;
-        FDLP_CHECK(m >= -kC4Guard && m < c4_item_stride(SL4));
-        const double v = img[m];
-        Bn[j] = m >= 0 ? v : 0.0;
+        FDLP_CHECK(k1c - li * SN - j >= -kC4Guard && k1c - li * SN - j < c4_item_stride(SL4));
+        Bn[j] = img[k1c - li * SN - j];
       }
       c4_durbin<SL4, SN>(An, Bn, R1n, part, E, rE, img, rrow, p, li, valid, r0, k1 + 1, cap, g);
       return;
@@ -885,6 +885,12 @@ __global__ __launch_bounds__(64, 2) void durbin4_kernel(const double* __restrict
   const bool valid = item < items;
   const double* rrow = r + (int64_t)(valid ? item : 0) * nlags;
   double* img = lds + kC4Guard + ii * kItem;
+  static_assert(4 * SL4 < kItem && kC4Guard >= 4 * kC4Step + 1, "zero margins of the select-free relayout");
+  {  // every image and the guard start at +0 (c4_durbin's relayout reads them instead of selecting zeros)
+    double2* z = reinterpret_cast<double2*>(lds);
+    static_assert((kC4Guard + 16 * kItem) % 2 == 0, "");
+    for (int q = lane; q < (kC4Guard + 16 * kItem) / 2; q += 64) z[q] = make_double2(0.0, 0.0);
+  }
   const double r0 = valid ? rrow[0] : 1.0;
   double A[1] = {li == 0 ? 1.0 : 0.0}, B[1] = {li == 0 ? 1.0 : 0.0};
   double R1[1] = {valid && li <= p ? rrow[li + 1] : 0.0};
