@@ -760,6 +760,8 @@ __device__ __forceinline__ double rcp_newton(double E) {
   return rE;
 }
 
+// one chain for the next order's dot product: its FMA latency stays below the 3 FMAs a position issues
+constexpr int kC4Chains = 1;
 template <int S>
 __device__ __forceinline__ void c4_step(double (&A)[S], double (&B)[S], const double (&R1)[S], double& part,
                                         double& E, double& rE) {
@@ -768,7 +770,7 @@ __device__ __forceinline__ void c4_step(double (&A)[S], double (&B)[S], const do
   // z B at slot 0: lane li - 1's last slot (row_shr:1; row edges take 0 from bound_ctrl, the other
   // quad edges the exact 0 of position 4 S - 1)
   const double z0 = __builtin_amdgcn_update_dpp(0.0, B[S - 1], 0x111, 0xF, 0xF, true);
-  constexpr int D = S >= 4 ? 2 : 1;  // dot-product chains
+  constexpr int D = kC4Chains;  // dot-product chains
   double pc[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) pc[d] = 0.0;
@@ -802,7 +804,7 @@ __device__ __forceinline__ bool k_done_ok(int p, int cap) { return p <= cap - 2;
 // ends at order p and leaves its A in img (positions < cap; exactly 0 past p), gg in g.
 template <int SL4, int S>
 __device__ __forceinline__ void c4_durbin(double (&A)[S], double (&B)[S], double (&R1)[S], double& part, double& E,
-                                          double& rE, double* img, const double* rrow, int p, int li, bool valid,
+                                          double& rE, double* img, const double* rl1, int plim, int p, int li,
                                           double r0, int k0, int& cap, double& g) {
   const int k1 = min(p, 4 * S - 2);
   constexpr int SN = S + kC4Step <= SL4 ? S + kC4Step : SL4;
@@ -813,10 +815,8 @@ __device__ __forceinline__ void c4_durbin(double (&A)[S], double (&B)[S], double
   if constexpr (SN > S) {
     if (k1 < p) {
 #pragma unroll
-      for (int t = 0; t < NA; ++t) {
-        const int m = 4 * S + li + 4 * t;
-        if (valid && m <= p) rn[t] = rrow[m + 1];
-      }
+      for (int t = 0; t < NA; ++t)
+        if (4 * S + 4 * t <= plim) rn[t] = rl1[4 * S + 4 * t];  // r_{m+1}, m = 4 S + li + 4 t <= p
     }
   }
   for (int k = k0; k <= k1; ++k) c4_step<S>(A, B, R1, part, E, rE);
@@ -852,7 +852,7 @@ __device__ __forceinline__ void c4_durbin(double (&A)[S], double (&B)[S], double
         FDLP_CHECK(k1c - li * SN - j >= -kC4Guard && k1c - li * SN - j < c4_item_stride(SL4));
         Bn[j] = img[k1c - li * SN - j];
       }
-      c4_durbin<SL4, SN>(An, Bn, R1n, part, E, rE, img, rrow, p, li, valid, r0, k1 + 1, cap, g);
+      c4_durbin<SL4, SN>(An, Bn, R1n, part, E, rE, img, rl1, plim, p, li, r0, k1 + 1, cap, g);
       return;
     }
   }
@@ -898,10 +898,26 @@ __global__ __launch_bounds__(64, 2) void durbin4_kernel(const double* __restrict
   double E = r0, rE = rcp_newton(r0);
   int cap = 0;
   double g = 0.0;
-  c4_durbin<SL4, 1>(A, B, R1, part, E, rE, img, rrow, p, li, valid, r0, 1, cap, g);
+  // the lane's r_{li+1} and its limit: position m = 4 S + li + 4 t is loaded while 4 S + 4 t <= p - li
+  const double* rl1 = rrow + 1 + li;
+  const int plim = valid ? p - li : -1;
+  c4_durbin<SL4, 1>(A, B, R1, part, E, rE, img, rl1, plim, p, li, r0, 1, cap, g);
   if (valid && li == 0) gg[item] = g;
   FDLP_CHECK(cap <= astride && cap <= c4_item_stride(SL4) && (cap & 1) == 0 && k_done_ok(p, cap));
   wave_lds_sync();
+  constexpr int kRow = 4 * SL4;  // a full image row (p = 4 SL4 - 2, the recipes' 150)
+  static_assert(kRow % 8 == 0 && kC4Guard % 2 == 0 && kItem % 2 == 0, "16-byte row pieces, 4 lanes per item");
+  if (cap == kRow) {  // wave-uniform: each quad copies its own item with immediate offsets, then the zero tail
+    FDLP_CHECK(astride >= kRow && (astride & 1) == 0);
+    if (valid) {
+      const double2* src = reinterpret_cast<const double2*>(img) + li;
+      double2* dst = reinterpret_cast<double2*>(a + (int64_t)item * astride) + li;
+#pragma unroll
+      for (int j = 0; j < kRow / 8; ++j) dst[4 * j] = src[4 * j];
+      for (int h = kRow / 2; h < (astride >> 1) - li; h += 4) dst[h] = make_double2(0.0, 0.0);
+    }
+    return;
+  }
   const int half = astride >> 1;
   for (int i = 0; i < 16; ++i) {
     if (item0 + i >= items) break;
