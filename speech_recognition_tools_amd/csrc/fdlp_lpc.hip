@@ -1192,16 +1192,22 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
     // S(u) = Even(u) + Odd(u), S(H - u) = Even(u) - Odd(u); lane slots cover u = 0..H/2 (lpc_env_kernel)
     for (int q0 = 0; q0 < TS; q0 += kEnvChunk) {
       double se[kEnvChunk], so[kEnvChunk], cprev[kEnvChunk], ccur[kEnvChunk], c2[kEnvChunk];
+      // slots u < 16 (q0 + kEnvChunk) <= env_nfft (every recipe: 80 <= 300) index the cosine table
+      // directly; the modulo (~16 integer instructions per slot) is compiled only into the other branch
+      auto setup = [&](auto direct) {
 #pragma unroll
-      for (int q = 0; q < kEnvChunk; ++q) {
-        const int u = l + 16 * (q0 + q);
-        const double c1 = A.env_cos[u % A.env_nfft];
-        se[q] = cw[0];
-        so[q] = 0.0;
-        cprev[q] = 1.0;
-        ccur[q] = c1;
-        c2[q] = 2.0 * c1;
-      }
+        for (int q = 0; q < kEnvChunk; ++q) {
+          const int u = l + 16 * (q0 + q);
+          const double c1 = A.env_cos[decltype(direct)::value ? u : u % A.env_nfft];
+          se[q] = cw[0];
+          so[q] = 0.0;
+          cprev[q] = 1.0;
+          ccur[q] = c1;
+          c2[q] = 2.0 * c1;
+        }
+      };
+      if (16 * (q0 + kEnvChunk) <= A.env_nfft) setup(std::true_type{});
+      else setup(std::false_type{});
       int n = 1;
       for (; n + 1 < ((FDLP_LPC_PHASES & 4) ? A.Me : 0); n += 2) {
         const double wo = cw[n], we = cw[n + 1];
