@@ -784,7 +784,7 @@ __device__ __forceinline__ void c4_step(double (&A)[S], double (&B)[S], const do
   }
   if constexpr (D == 2) part = pc[0] + pc[1];
   else part = pc[0];
-  E = E * (1.0 - kappa * kappa);
+  E = fma(kappa, acc, E);  // E (1 - kappa^2) with kappa = -acc / E, one FMA
   rE = rcp_newton(E);
 }
 
