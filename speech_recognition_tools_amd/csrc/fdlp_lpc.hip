@@ -943,6 +943,14 @@ constexpr int kEnvChunk = 5;  // envelope slots held in registers at a time
 // DM: the Durbin phase.  1: the contiguous-chunk Durbin (contig_durbin, p outside durbin8_kernel's
 // range); 2: none, a and gg come from durbin8_kernel (A.a_ext, A.gg_ext; default where it is instantiated).
 constexpr int kDmContig = 1, kDmExt = 2;
+// 1/n for a count n >= 1: v_rcp_f64 and two Newton steps, within an ulp of the quotient (the cepstrum's
+// c_n = d_n / n once per coefficient; an IEEE division is ~10 instructions)
+__device__ __forceinline__ double inv_count(int n) {
+  const double x = (double)n;
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return fma(r, fma(-x, r, 1.0), r);
+}
 // waves per SIMD the lattice kernel is compiled for (register budget).  CB > 0: 4 (127 VGPRs and 12 spilled
 // once per group: 0.62 ms per 327 680 items against 0.68 at 3 waves without spills, r04d); the super-block
 // cepstrum (CB < 0) holds ~70 doubles of window, H rows and accumulators (spills at 3 waves per SIMD); its
@@ -1065,7 +1073,7 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
         const double an = n <= p ? la[min(n, p)] : 0.0;
         const double y = -(double)n * an - ((a0 + a1) + (a2 + a3));
         const double d = sb_solve(y, Hrow);
-        const double mine = n == 0 ? log(sqrt(gg)) : d * (1.0 / (double)(n > 0 ? n : 1));
+        const double mine = n == 0 ? log(sqrt(gg)) : d * inv_count(n > 0 ? n : 1);
         kc[b] = d;  // 0 for n = 0 (y_0 = 0)
         if (n < CSN) cs[n] = mine;
         if (n < M && valid && A.cep_out) A.cep_out[(int64_t)item * M + n] = mine;
@@ -1118,7 +1126,7 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
           const double y = -(double)n * an - (acc[r][0] + acc[r][1]);
           const double d = sb_solve(y, Hrow);
           kcnew[r] = d;
-          const double c = n == 0 ? log(sqrt(gg)) : d * (1.0 / (double)(n > 0 ? n : 1));
+          const double c = n == 0 ? log(sqrt(gg)) : d * inv_count(n > 0 ? n : 1);
           if (n < CSN) cs[n] = c;
           if (n < M && valid && A.cep_out) A.cep_out[(int64_t)item * M + n] = c;
           asm volatile("s_nop 1");  // kcnew[r] feeds the next block's DPP-broadcast FMAs
