@@ -55,8 +55,12 @@ __global__ __launch_bounds__(256) void ola_log_tiled_kernel(DevConsts c, const d
     }
     __syncthreads();
   }
+  // t = q / B by a float reciprocal: (q + 0.5) / B sits at least 0.5 / B from an integer, and two float
+  // roundings move it by at most (q / B) 2^-22 <= kOlaRows 2^-22, far less for any B below 65536
+  const float invB = 1.0f / (float)B;
   for (int q = tid; q < nt * B; q += blockDim.x) {
-    const int t = q / B, j = q - t * B;
+    const int t = (int)(((float)q + 0.5f) * invB), j = q - t * B;
+    FDLP_CHECK(t >= 0 && t < nt && j >= 0 && j < B);
     const double acc = tile[t * BS + j];
     const double v = log(acc < 1e-14 ? 1e-14 : acc);  // np.clip(a_min=1e-14) keeps NaN; :227
     const int64_t o = (U.out_row + t0 + t) * (int64_t)B + j;
