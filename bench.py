@@ -404,7 +404,8 @@ def combine_xfer_children(got):
     x["audio_h"] = sum(g["audio_h"] for g in got)
     x["elapsed_s"] = max(g["elapsed_s"] for g in got)
     x["per_rank_value"] = [g["value"] for g in got]
-    x.pop("mapped_output", None)
+    for k in ("float32_d2h", "mapped_codes"):
+        x.pop(k, None)
     x["note"] = (x.get("note", "") + "; one child process per rank on its own GPU, started before the rank "
                  "touches it, all at once: value = total audio / the slowest child's time")
     return x
@@ -440,6 +441,120 @@ def host_cores():
     return max(1, min(n, int(share))) if share.isdigit() and int(share) > 0 else max(1, n)
 
 
+def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, audio_s, world, dd, sync, dev, B):
+    """SURVEY.md 8(d) wall, first H2D to last D2H: every batch's PCM copied in from pinned host memory and
+    its features copied back to pinned host memory, every batch of every step.  Every batch in flight has
+    two device buffer sets used on alternate steps, so step s + 1's copy-in runs while step s computes and
+    step s's copy-out while step s + 1 computes (with one set per batch, every step's four copy-ins queued
+    behind the previous step's kernels on the one H2D stream: 31.9 ms per step against 23.4 computing,
+    r03f).  One H2D stream, --xfer-d2h-streams D2H streams; the compute of batch b stays on its own stream.
+
+    The features leave the device as the compact ark codes (ABI 7, include/fdlp.h out_q_dev): int16
+    k = nearbyint(v 10^3) per value, the ark's float32 (float)(k / 10^3) restored bit for bit on the host by
+    fdlp_q_widen (the flag word of the batch, copied back with the codes, says whether every value had a
+    code; otherwise the batch's float32 rows, also written in HBM, are the ones to fetch).  Variants, same
+    steps: `float32_d2h` copies the float32 rows instead (ABI 6 protocol, twice the D2H bytes);
+    `mapped_codes`: the OLA kernel stores the codes straight into pinned host memory (no D2H copy)."""
+    import torch
+    from speech_recognition_tools_amd import q_widen
+    out = outs[0]
+    rows, D = out.shape
+    nq = rows * D
+    pin_in = torch.from_numpy(pcm_host).pin_memory()
+    NB = 2 * B                                       # device buffer sets: (batch, step parity)
+    pcm_d = [pcms[i // 2] if i % 2 == 0 else torch.empty_like(pcms[0]) for i in range(NB)]
+    out_d = [outs[i // 2] if i % 2 == 0 else torch.empty_like(out) for i in range(NB)]
+    # codes + the flag word in one buffer: [nq int16 codes | int32 flag], one D2H copy per batch
+    q_d = [torch.empty(nq + 2, dtype=torch.int16, device=dev) for _ in range(NB)]
+    q_h = [torch.empty(nq + 2, dtype=torch.int16).pin_memory() for _ in range(NB)]
+    out_h = [torch.empty(out.shape, dtype=out.dtype).pin_memory() for _ in range(NB)]
+    s_in = torch.cuda.Stream(dev)
+    nd = args.xfer_d2h_streams or (2 if args.xfer_only else 1)
+    s_outs = [torch.cuda.Stream(dev) for _ in range(nd)]
+    nc = args.xfer_compute_streams or B
+    comp = [torch.cuda.current_stream(dev)] if B == 1 else [streams[b % nc] for b in range(B)]
+    ev_in = [torch.cuda.Event() for _ in range(NB)]
+    ev_done = [torch.cuda.Event() for _ in range(NB)]
+    ev_out = [torch.cuda.Event() for _ in range(NB)]
+    for i in range(NB):
+        ev_done[i].record(comp[(i // 2) % len(comp)])
+        ev_out[i].record(comp[(i // 2) % len(comp)])
+    it = [0]
+    mode = ["codes"]
+
+    def xbatch(b, i):
+        cs = comp[b % len(comp)]
+        s_in.wait_event(ev_done[i])                  # pcm_d[i] no longer read by its previous compute
+        with torch.cuda.stream(s_in):
+            pcm_d[i].copy_(pin_in, non_blocking=True)
+            ev_in[i].record(s_in)
+        cs.wait_event(ev_in[i])
+        cs.wait_event(ev_out[i])                     # out_d[i] / q_d[i] copied out by its previous D2H
+        with torch.cuda.stream(cs):
+            if mode[0] == "float32":
+                plans[b].compute(pcm_d[i], lens, rng.randbits2(nj), out=out_d[i], **mix[b])
+            else:
+                qt = q_h[i] if mode[0] == "mapped" else q_d[i]
+                flag = qt[nq:].view(torch.int32)
+                flag.zero_()
+                plans[b].compute(pcm_d[i], lens, rng.randbits2(nj), out=out_d[i], out_q=qt[:nq].view(rows, D),
+                                 q_flag=flag, **mix[b])
+            ev_done[i].record(cs)
+        if mode[0] == "mapped":
+            ev_out[i].record(cs)
+            return
+        so = s_outs[b % nd]
+        so.wait_event(ev_done[i])
+        with torch.cuda.stream(so):
+            if mode[0] == "float32":
+                out_h[i].copy_(out_d[i], non_blocking=True)
+            else:
+                q_h[i].copy_(q_d[i], non_blocking=True)
+            ev_out[i].record(so)
+
+    def xstep():
+        par = it[0] & 1
+        it[0] += 1
+        for b in range(B):
+            xbatch(b, 2 * b + par)
+
+    cpu_dev = torch.device("cpu")
+    from speech_recognition_tools_amd.shard import timed_steps
+    el_x = timed_steps(xstep, args.steps, args.warmup, sync, dd, cpu_dev)
+    flags = [int(q[nq:].view(torch.int32)[0]) for q in q_h]
+    # the codes of the last steps' batches widen to the float32 rows still in HBM (bit-identical)
+    par = (it[0] - 1) & 1
+    wid = q_widen(q_h[par][:nq], 3, threads=16).reshape(rows, D)
+    same = bool(np.array_equal(wid.view(np.uint32), out_d[par].cpu().numpy().view(np.uint32)))
+    t0 = time.perf_counter()
+    for i in range(B):                               # host cost of the widening, one step's codes
+        q_widen(q_h[i][:nq], 3, threads=16, out=out_h[i].numpy().reshape(-1))
+    widen_s = time.perf_counter() - t0
+    ah = world * args.steps * B * audio_s / 3600.0
+    el_v = {}
+    for v in ("float32", "mapped"):
+        if v in args.xfer_variants.split(","):
+            mode[0] = v
+            el_v[v] = timed_steps(xstep, args.steps, 1, sync, dd, cpu_dev)
+    variant = lambda v, d: dict(value=ah / el_v[v], ms_per_step=el_v[v] / args.steps * 1e3, **d) if v in el_v else None
+    return {"value": ah / el_x, "ms_per_step": el_x / args.steps * 1e3, "audio_h": ah, "elapsed_s": el_x,
+            "h2d_bytes_per_step": int(B * pcm_host.nbytes), "d2h_bytes_per_step": int(B * (nq + 2) * 2),
+            "d2h_encoding": "compact ark codes: int16 nearbyint(v * 1e3) + an int32 flag per batch (ABI 7)",
+            "codes_flagged_batches": sum(1 for f in flags if f), "codes_widen_bit_identical": same,
+            "host_widen_ms_per_step": widen_s * 1e3,
+            "host_widen_note": "fdlp_q_widen of one step's codes to float32 on 16 host threads (after the timed "
+                               "region: the float32 values an ark writer needs, outside 8(d)'s H2D..D2H wall)",
+            "float32_d2h": variant("float32", {"d2h_bytes_per_step": int(B * out.numel() * 4),
+                                               "note": "the same steps copying the float32 rows back (ABI 6 "
+                                                       "protocol)"}),
+            "mapped_codes": variant("mapped", {"note": "the OLA kernel stores the codes straight into pinned host "
+                                                       "memory (fdlp_mapped_ptr) instead of a D2H copy"}),
+            "note": "every batch's PCM copied in from pinned host memory and its compact feature codes copied "
+                    "back every step (%d batch(es) in flight on %d compute stream(s), two device buffer sets per "
+                    "batch on alternate steps, one H2D stream, %d D2H stream(s)); not the headline (inputs "
+                    "resident in HBM)" % (B, len(comp), nd)}
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -462,6 +577,8 @@ def parse_args(argv=None):
                     help="PCIe pass: every rank runs it in a child process (started before the rank touches the "
                          "GPU) with GPU_MAX_HW_QUEUES set to this (the compute, H2D and D2H streams then get hardware "
                          "queues of their own; 0: in-process, with the process default of 4)")
+    ap.add_argument("--xfer-variants", default="float32,mapped",
+                    help="PCIe pass: the variants timed after the compact-code pass (float32 D2H, mapped codes)")
     ap.add_argument("--xfer-only", action="store_true", help=argparse.SUPPRESS)  # the PCIe-pass child
     ap.add_argument("--xfer-shard", default=None, help=argparse.SUPPRESS)  # rank/world of the child's shard
     ap.add_argument("--xfer-compute-streams", type=int, default=0,
@@ -661,68 +778,8 @@ def main():
         xfer_child = combine_xfer_children(got)
     xfer = xfer_child
     if not args.no_transfers and xfer_child is None:
-        pin_in = torch.from_numpy(pcm_host).pin_memory()
-        NB = 2 * B                                       # device buffer sets: (batch, step parity)
-        pcm_d = [pcms[i // 2] if i % 2 == 0 else torch.empty_like(pcm) for i in range(NB)]
-        out_d = [outs[i // 2] if i % 2 == 0 else torch.empty_like(out) for i in range(NB)]
-        out_h = [torch.empty(out.shape, dtype=out.dtype).pin_memory() for _ in range(NB)]
-        # streams: H2D, D2H (--xfer-d2h-streams, batch b on b mod that) and compute (--xfer-compute-streams,
-        # default one per batch in flight)
-        s_in = torch.cuda.Stream(dev)
-        nd = args.xfer_d2h_streams or (2 if args.xfer_only else 1)
-        s_outs = [torch.cuda.Stream(dev) for _ in range(nd)]
-        nc = args.xfer_compute_streams or B
-        comp = [torch.cuda.current_stream(dev)] if B == 1 else [streams[b % nc] for b in range(B)]
-        ev_in = [torch.cuda.Event() for _ in range(NB)]
-        ev_done = [torch.cuda.Event() for _ in range(NB)]
-        ev_out = [torch.cuda.Event() for _ in range(NB)]
-        for i in range(NB):
-            ev_done[i].record(comp[(i // 2) % len(comp)])
-            ev_out[i].record(comp[(i // 2) % len(comp)])
-        it = [0]
-        mapped = [False]
-
-        def xbatch(b, i):
-            cs = comp[b % len(comp)]
-            s_in.wait_event(ev_done[i])                  # pcm_d[i] no longer read by its previous compute
-            with torch.cuda.stream(s_in):
-                pcm_d[i].copy_(pin_in, non_blocking=True)
-                ev_in[i].record(s_in)
-            cs.wait_event(ev_in[i])
-            cs.wait_event(ev_out[i])                     # out_d[i] copied out by its previous D2H
-            with torch.cuda.stream(cs):
-                plans[b].compute(pcm_d[i], lens, rng.randbits2(nj), out=out_h[i] if mapped[0] else out_d[i],
-                                 **mix[b])
-                ev_done[i].record(cs)
-            if mapped[0]:
-                ev_out[i].record(cs)
-                return
-            so = s_outs[b % nd]
-            so.wait_event(ev_done[i])
-            with torch.cuda.stream(so):
-                out_h[i].copy_(out_d[i], non_blocking=True)
-                ev_out[i].record(so)
-
-        def xstep():
-            par = it[0] & 1
-            it[0] += 1
-            for b in range(B):
-                xbatch(b, 2 * b + par)
-
-        el_x = timed_steps(xstep, args.steps, args.warmup, sync, dd, cpu_dev)
-        mapped[0] = True
-        el_m = timed_steps(xstep, args.steps, 1, sync, dd, cpu_dev)
-        xfer = {"value": world * args.steps * B * audio_s / 3600.0 / el_x, "ms_per_step": el_x / args.steps * 1e3,
-                "audio_h": world * args.steps * B * audio_s / 3600.0, "elapsed_s": el_x,
-                "h2d_bytes_per_step": int(B * pcm_host.nbytes), "d2h_bytes_per_step": int(B * out.numel() * 4),
-                "mapped_output": {"value": world * args.steps * B * audio_s / 3600.0 / el_m,
-                                  "ms_per_step": el_m / args.steps * 1e3,
-                                  "note": "features stored by the OLA kernel straight into pinned host memory "
-                                          "(fdlp_mapped_ptr) instead of the D2H copy"},
-                "note": "every batch's PCM copied in from pinned host memory and its float32 features copied back "
-                        "every step (%d batch(es) in flight on %d compute stream(s), two device buffer sets per "
-                        "batch on alternate steps, one H2D stream, %d D2H stream(s)); not the headline (inputs "
-                        "resident in HBM)" % (B, len(comp), nd)}
+        xfer = pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, audio_s, world, dd,
+                         sync, dev, B)
 
     if args.xfer_only:
         xfer["hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES", "default")

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define FDLP_ABI_VERSION 6
+#define FDLP_ABI_VERSION 7
 
 enum {
   FDLP_OK = 0,
@@ -100,6 +100,16 @@ typedef struct fdlp_batch {
                                     features.py:66 uses 3); <0: keep full float32               */
   int32_t preprocess;            /* FDLP_PRE_DIFF: x = convolve(int16 s, [1,2,3,2,0,-2,-5,-2,0,2,3,
                                     2,1], 'same') on the device (int16 PCM only)                 */
+  /* ABI 7: compact ark codes, half the bytes of out_dev for the device-to-host leg.  With
+     ark_decimals = d >= 0 the ark value of a feature is the float32 (float)(k / 10^d) with
+     k = nearbyint(v * 10^d) (dict2Ark's '%.3f' text read back by copy-feats, features.py:66).
+     out_q_dev receives k as int16 (-32768 = -0.0), same layout as out_dev; fdlp_q_widen turns the
+     codes into exactly the float32 values out_dev would hold.  A value without a code (|k| > 32767
+     or NaN; log features of 16-bit audio stay within [-32.24, +19]) stores -32768 and writes 1 to
+     *out_q_flag_dev, which the caller zeroes before the call: that batch's float32 rows (out_dev,
+     when also given) are then the ones to use.  Spectrogram plans only.                          */
+  int16_t* out_q_dev;            /* nullable device [sum_u L_u, nfilters] int16 codes               */
+  uint32_t* out_q_flag_dev;      /* device word, required with out_q_dev                            */
 } fdlp_batch;
 
 /* ---- plan ------------------------------------------------------------------------------- */
@@ -142,6 +152,9 @@ int fdlp_ola_table(const fdlp_plan* plan, int64_t T, const uint8_t* jitter, int3
 /* Whole pipeline for a batch (getFeats :159-229).  Enqueued on `stream`; host arrays are
  * consumed before return. */
 int fdlp_compute(fdlp_plan* plan, const fdlp_batch* batch, void* stream);
+/* Host: the float32 ark values of n compact codes (fdlp_batch.out_q_dev) with the batch's ark_decimals,
+ * bit-identical to the float32 out_dev rows; `threads` > 1 splits the work (ABI 7). */
+int fdlp_q_widen(const int16_t* q, int64_t n, int32_t decimals, float* out, int32_t threads);
 /* Keep the fused LPC kernel's a/gg/cep in the workspace (off by default; needed by
  * fdlp_debug_fetch for those three arrays). */
 int fdlp_set_debug(fdlp_plan* plan, int32_t keep_intermediates);

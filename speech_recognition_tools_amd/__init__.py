@@ -13,7 +13,7 @@ import importlib
 import sys
 
 _LAZY = {"FdlpPlan": ".plan", "FeatureConfig": ".config", "DEFAULT_SUPPORT_EPS": ".config",
-         "PyRandom": ".rng", "NpRandom": ".rng", "FdlpError": "._lib", "lib": "._lib"}
+         "PyRandom": ".rng", "NpRandom": ".rng", "FdlpError": "._lib", "lib": "._lib", "q_widen": ".plan"}
 
 __all__ = ["FdlpPlan", "FeatureConfig", "PyRandom", "NpRandom", "FdlpError", "DEFAULT_SUPPORT_EPS"]
 

@@ -39,6 +39,7 @@ FDLP_MODE_MODSPEC_COMPLEX = 2
 FDLP_WIN_HAMMING = 0
 FDLP_WIN_HANNING = 1
 FDLP_WIN_RECT = 2
+ABI_VERSION = 7
 STAGE_NAMES = ("frames_dft1", "dft2_dct", "autocorr", "lpc_env", "ola_log")
 
 c_i32, c_i64, c_dbl, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
@@ -69,7 +70,7 @@ class FdlpBatchC(ctypes.Structure):
         ("n_utt", c_i32), ("pcm_kind", c_i32), ("pcm_dev", c_p), ("pcm_off", P_i64),
         ("utt_len", P_i64), ("jitter", P_u8), ("noise_dev", c_p), ("noise_off", P_i64),
         ("noise_alpha", P_dbl), ("out_dev", c_p), ("out_row", P_i64), ("out_f64_dev", c_p),
-        ("ark_decimals", c_i32), ("preprocess", c_i32),
+        ("ark_decimals", c_i32), ("preprocess", c_i32), ("out_q_dev", c_p), ("out_q_flag_dev", c_p),
     ]
 
 
@@ -122,6 +123,7 @@ SIGNATURES = {
     "fdlp_make_fbank": (c_i32, [ctypes.POINTER(FdlpConfigC), c_i32, P_dbl, P_i32]),
     "fdlp_ola_table": (c_i32, [c_p, c_i64, P_u8, P_i32, P_i32, P_i32]),
     "fdlp_compute": (c_i32, [c_p, ctypes.POINTER(FdlpBatchC), c_p]),
+    "fdlp_q_widen": (c_i32, [c_p, c_i64, c_i32, c_p, c_i32]),
     "fdlp_debug_fetch": (c_i32, [c_p, c_i32, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl]),
     "fdlp_debug_fetch_range": (c_i32, [c_p, c_i32, c_i32, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl, P_dbl]),
     "fdlp_set_profiling": (c_i32, [c_p, c_i32]),
@@ -184,7 +186,7 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.fdlp_abi_version() != 6:
+    if lib.fdlp_abi_version() != ABI_VERSION:
         raise ImportError("libfdlp_hip.so ABI mismatch")
     return lib
 

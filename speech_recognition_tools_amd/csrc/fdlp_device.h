@@ -280,6 +280,22 @@ __device__ __forceinline__ void bfly_c(double2 (&v)[R]) {
 }
 
 
+// -----------------------------------------------------------------------------------------
+// Compact ark codes (ABI 7).  dict2Ark writes '%.3f' text (features.py:66) that copy-feats reads back
+// as float32; on the device that value is (float)(k / 10^d) with k = nearbyint(v 10^d).  The integer k
+// fits int16 for every log feature the recipes produce (log(1e-14) = -32.236 is the floor, full-scale
+// int16 input peaks near +18), so the features can leave the device as 2-byte codes and be widened
+// bit-exactly on the host (fdlp_q_widen): code = k, except -32768 = -0.0 (k = -0 keeps its sign through
+// the division).  A value without a code (|k| > 32767, NaN) stores -32768 and sets *flag (plain vector
+// store); the caller then takes that batch's float32 rows instead.
+// -----------------------------------------------------------------------------------------
+constexpr int16_t kQNegZero = -32768;
+__device__ __forceinline__ int16_t q_code(double k, bool& bad) {
+  if (k >= -32767.0 && k <= 32767.0) return (k == 0.0 && signbit(k)) ? kQNegZero : (int16_t)(int)k;
+  bad = true;  // out of range or NaN
+  return kQNegZero;
+}
+
 // numpy 'reflect' padding index (getFrames, features.py:146)
 __device__ __forceinline__ int64_t reflect_idx(int64_t q, int64_t T) {
   // numpy 'reflect' pad == periodic reflection with period 2(T-1) (features.py:146); the 64-bit

@@ -19,6 +19,8 @@
 #include <algorithm>
 #include <new>
 #include <string>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/fdlp.h"
@@ -152,6 +154,52 @@ int fdlp_noise_params(const int16_t* sig, int64_t T, const int16_t* noise, int64
   const double Es = (double)es / (double)T, En = (double)en / (double)T;
   *alpha = sqrt(Es / (En * pow(10.0, snr / 10.0)));  // (features.py:29)
   *off = o;
+  return FDLP_OK;
+}
+
+// Compact ark codes -> the float32 ark values (fdlp_batch.out_q_dev, fdlp_device.h q_code): the device
+// stores (float)(k / 10^d) in out_dev; here the same two IEEE operations on the same k, so the floats
+// are bitwise the ones the device would have written.  -32768 is -0.0.  The 65536 values of a decimals
+// setting are computed once into a table (a lookup per code instead of a double division).
+static float q_value(int k, double scale10) { return k == -32768 ? -0.0f : (float)((double)k / scale10); }
+
+static const float* q_table(int decimals, double scale10) {
+  constexpr int kTables = 10;
+  static std::once_flag once[kTables];
+  static std::vector<float> tab[kTables];
+  if (decimals >= kTables) return nullptr;
+  std::call_once(once[decimals], [&] {
+    tab[decimals].resize(65536);
+    for (int k = -32768; k < 32768; ++k) tab[decimals][k + 32768] = q_value(k, scale10);
+  });
+  return tab[decimals].data();
+}
+
+static void q_widen_range(const int16_t* q, int64_t n, const float* lut, double scale10, float* out) {
+  if (lut) {
+    for (int64_t i = 0; i < n; ++i) out[i] = lut[(int)q[i] + 32768];
+  } else {
+    for (int64_t i = 0; i < n; ++i) out[i] = q_value(q[i], scale10);
+  }
+}
+
+int fdlp_q_widen(const int16_t* q, int64_t n, int32_t decimals, float* out, int32_t threads) {
+  if (n < 0 || (n > 0 && (!q || !out)) || decimals < 0) return fdlp::fail(FDLP_E_INVALID, "fdlp_q_widen: bad args");
+  double scale10 = 1.0;
+  for (int i = 0; i < decimals; ++i) scale10 *= 10.0;  // as launch_ola_log
+  const float* lut = n >= 4096 ? q_table(decimals, scale10) : nullptr;
+  const int64_t nt = std::max<int64_t>(1, std::min<int64_t>(threads, n / (int64_t(1) << 16)));
+  if (nt <= 1) {
+    q_widen_range(q, n, lut, scale10, out);
+    return FDLP_OK;
+  }
+  std::vector<std::thread> th;
+  for (int64_t t = 1; t < nt; ++t) {
+    const int64_t a = n * t / nt, b = n * (t + 1) / nt;
+    th.emplace_back(q_widen_range, q + a, b - a, lut, scale10, out + a);
+  }
+  q_widen_range(q, n / nt, lut, scale10, out);
+  for (auto& x : th) x.join();
   return FDLP_OK;
 }
 

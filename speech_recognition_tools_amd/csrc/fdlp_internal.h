@@ -160,7 +160,7 @@ hipError_t launch_cplx_modspec(const DevConsts& c, int L, const double* X, int n
                                int decimals, hipStream_t s);
 hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc* frames,
                           const UttDesc* utts, int n_utt, int maxL, float* out,
-                          double* out_f64, int decimals, hipStream_t s);
+                          double* out_f64, int16_t* out_q, uint32_t* q_flag, int decimals, hipStream_t s);
 // Mel spectrum (computeMelSpectrum.py): one analysis frame and the plan constants.
 struct MelFrame {
   int64_t pcm_off, noise_off;  // noise_off < 0: no mixing

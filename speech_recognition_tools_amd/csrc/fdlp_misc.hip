@@ -24,7 +24,8 @@ constexpr int kOlaRows = 32;
 __global__ __launch_bounds__(256) void ola_log_tiled_kernel(DevConsts c, const double* __restrict__ env,
                                                             const FrameDesc* __restrict__ frames,
                                                             const UttDesc* __restrict__ utts, float* __restrict__ out,
-                                                            double* __restrict__ out64, int decimals, double scale10) {
+                                                            double* __restrict__ out64, int16_t* __restrict__ outq,
+                                                            uint32_t* __restrict__ qflag, int decimals, double scale10) {
   extern __shared__ double tile[];  // [kOlaRows][B + 1]
   const int u = blockIdx.y;
   const UttDesc U = utts[u];
@@ -58,6 +59,7 @@ __global__ __launch_bounds__(256) void ola_log_tiled_kernel(DevConsts c, const d
   // t = q / B by a float reciprocal: (q + 0.5) / B sits at least 0.5 / B from an integer, and two float
   // roundings move it by at most (q / B) 2^-22 <= kOlaRows 2^-22, far less for any B below 65536
   const float invB = 1.0f / (float)B;
+  bool bad = false;
   for (int q = tid; q < nt * B; q += blockDim.x) {
     const int t = (int)(((float)q + 0.5f) * invB), j = q - t * B;
     FDLP_CHECK(t >= 0 && t < nt && j >= 0 && j < B);
@@ -65,22 +67,27 @@ __global__ __launch_bounds__(256) void ola_log_tiled_kernel(DevConsts c, const d
     const double v = log(acc < 1e-14 ? 1e-14 : acc);  // np.clip(a_min=1e-14) keeps NaN; :227
     const int64_t o = (U.out_row + t0 + t) * (int64_t)B + j;
     if (out64) out64[o] = v;
-    if (out) out[o] = decimals >= 0 ? (float)(nearbyint(v * scale10) / scale10) : (float)v;
+    const double k = nearbyint(v * scale10);
+    if (out) out[o] = decimals >= 0 ? (float)(k / scale10) : (float)v;
+    if (outq) outq[o] = q_code(k, bad);
   }
+  if (bad) *qflag = 1u;
 }
 
 
 hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc* frames, const UttDesc* utts,
-                          int n_utt, int maxL, float* out, double* out_f64, int decimals, hipStream_t s) {
+                          int n_utt, int maxL, float* out, double* out_f64, int16_t* out_q, uint32_t* q_flag,
+                          int decimals, hipStream_t s) {
   if (n_utt <= 0 || maxL <= 0) return hipSuccess;
+  if (out_q && (decimals < 0 || !q_flag)) return hipErrorInvalidValue;
   double scale10 = 1.0;
   for (int i = 0; i < decimals; ++i) scale10 *= 10.0;
   dim3 grid((unsigned)((maxL + kOlaRows - 1) / kOlaRows), n_utt);
   const size_t lds = sizeof(double) * kOlaRows * (size_t)(c.B + 1);
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)ola_log_tiled_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(ola_log_tiled_kernel, grid, dim3(256), lds, s, c, env, frames, utts, out, out_f64, decimals,
-                     scale10);
+  hipLaunchKernelGGL(ola_log_tiled_kernel, grid, dim3(256), lds, s, c, env, frames, utts, out, out_f64, out_q, q_flag,
+                     decimals, scale10);
   return hipGetLastError();
 }
 

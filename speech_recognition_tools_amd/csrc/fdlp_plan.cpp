@@ -919,7 +919,9 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
   if (b->preprocess != FDLP_PRE_NONE && b->preprocess != FDLP_PRE_DIFF) return fail(FDLP_E_INVALID, "bad preprocess");
   if (b->preprocess == FDLP_PRE_DIFF && (b->pcm_kind != FDLP_PCM_I16 || b->noise_dev))
     return fail(FDLP_E_INVALID, "diff preprocessing needs int16 PCM and no noise mixing");
-  if (!b->out_dev && !b->out_f64_dev) return fail(FDLP_E_INVALID, "fdlp_compute: no output buffer");
+  if (!b->out_dev && !b->out_f64_dev && !b->out_q_dev) return fail(FDLP_E_INVALID, "fdlp_compute: no output buffer");
+  if (b->out_q_dev && (b->ark_decimals < 0 || !b->out_q_flag_dev || p->modspec))
+    return fail(FDLP_E_INVALID, "fdlp_compute: out_q_dev needs ark_decimals >= 0, out_q_flag_dev and a spectrogram plan");
   if (p->device < 0) return fail(FDLP_E_INVALID, "fdlp_compute: host-only plan (created with device < 0)");
   hipStream_t s = (hipStream_t)stream;
   DeviceGuard dg(p->device);  // the caller's current device is restored on return
@@ -1060,7 +1062,7 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
                                      c.absolute_value, b->out_dev, b->out_f64_dev, b->ark_decimals, s));
   } else if (!p->modspec) {  // (complex modulation: the rows were written by launch_cplx_modspec)
     HIP_TRY(fdlp::launch_ola_log(p->dc, p->ws.env, p->d_frames, p->d_utts, b->n_utt, maxL, b->out_dev,
-                                 b->out_f64_dev, b->ark_decimals, s));
+                                 b->out_f64_dev, b->out_q_dev, b->out_q_flag_dev, b->ark_decimals, s));
   }
   if (p->profiling) {
     HIP_TRY(hipEventRecord(ev.back(), s));

@@ -90,10 +90,16 @@ class FdlpPlan:
                 offsets: Optional[Sequence[int]] = None, noise: Optional[torch.Tensor] = None,
                 noise_off: Optional[Sequence[int]] = None, noise_alpha: Optional[Sequence[float]] = None,
                 ark_decimals: int = 3, want_f64: bool = False, out: Optional[torch.Tensor] = None,
-                stream: Optional[torch.cuda.Stream] = None, preprocess: Optional[str] = None):
+                stream: Optional[torch.cuda.Stream] = None, preprocess: Optional[str] = None,
+                out_q: Optional[torch.Tensor] = None, q_flag: Optional[torch.Tensor] = None):
         """Features of a batch of utterances whose samples are concatenated in ``pcm`` (device).
 
-        Returns (feats float32 [sum L, B], row offsets int64 [n_utt+1], feats_f64 or None)."""
+        ``out_q`` (int16 [>= sum L, B], device or pinned host) receives the compact ark codes (ABI 7,
+        include/fdlp.h): ``q_widen`` turns them into the float32 rows bit for bit; ``q_flag`` (int32
+        device or pinned tensor, zeroed by the caller) becomes non-zero when a value has no code.  With
+        ``out_q`` and no ``out`` no float32 rows are written.
+
+        Returns (feats float32 [sum L, B] or None, row offsets int64 [n_utt+1], feats_f64 or None)."""
         if not pcm.is_cuda:
             raise ValueError("pcm must be a device tensor")
         if pcm.dtype == torch.int16:
@@ -119,10 +125,17 @@ class FdlpPlan:
         total = int(rows[-1])
         dev = pcm.device
         D = self.out_dim
-        if out is None:
+        if out is None and out_q is None:
             out = torch.empty((total, D), dtype=torch.float32, device=dev)
-        elif out.shape[0] < total or out.shape[1] != D or out.dtype != torch.float32 or not out.is_contiguous():
+        elif out is not None and (out.shape[0] < total or out.shape[1] != D or out.dtype != torch.float32
+                                  or not out.is_contiguous()):
             raise ValueError("out buffer too small")
+        if out_q is not None:
+            if (out_q.dtype != torch.int16 or out_q.dim() != 2 or out_q.shape[0] < total or out_q.shape[1] != D
+                    or not out_q.is_contiguous()):
+                raise ValueError("out_q must be a contiguous int16 [>= sum L, out_dim] tensor")
+            if q_flag is None or q_flag.dtype != torch.int32 or q_flag.numel() < 1:
+                raise ValueError("out_q needs q_flag (an int32 tensor of at least one element)")
         out64 = torch.empty((total, D), dtype=torch.float64, device=dev) if want_f64 else None
         jit = np.ascontiguousarray(np.zeros(1) if jitter is None else jitter, dtype=np.uint8)
         b = FdlpBatchC()
@@ -136,14 +149,9 @@ class FdlpPlan:
             na = np.ascontiguousarray(np.asarray(noise_alpha, dtype=np.float64))
             keep += [no, na]
             b.noise_dev, b.noise_off, b.noise_alpha = noise.data_ptr(), ptr(no, ctypes.c_int64), ptr(na, ctypes.c_double)
-        if out.is_cuda:
-            b.out_dev = out.data_ptr()
-        elif out.is_pinned():  # the OLA kernel stores into pinned host memory through its device mapping
-            dp = ctypes.c_void_p()
-            check(lib.fdlp_mapped_ptr(ctypes.c_void_p(out.data_ptr()), ctypes.byref(dp)))
-            b.out_dev = dp.value
-        else:
-            raise ValueError("out must be a device tensor or a pinned host tensor")
+        b.out_dev = _dev_ptr(out, "out") if out is not None else None
+        if out_q is not None:
+            b.out_q_dev, b.out_q_flag_dev = _dev_ptr(out_q, "out_q"), _dev_ptr(q_flag, "q_flag")
         rows_c = np.ascontiguousarray(rows[:-1])
         b.out_row = ptr(rows_c, ctypes.c_int64)
         b.out_f64_dev = out64.data_ptr() if out64 is not None else None
@@ -153,7 +161,7 @@ class FdlpPlan:
         b.preprocess = _lib.FDLP_PRE_DIFF if preprocess == "diff" else _lib.FDLP_PRE_NONE
         s = stream if stream is not None else torch.cuda.current_stream(dev)
         check(lib.fdlp_compute(self._h, ctypes.byref(b), ctypes.c_void_p(s.cuda_stream)))
-        return out[:total], rows, out64
+        return (out[:total] if out is not None else None), rows, out64
 
     AUTOCORR_PATHS = {"auto": 0, "direct": 1, "structured": 2, "structured_mfma": 3}
 
@@ -267,6 +275,30 @@ class FdlpPlan:
         check(lib.fdlp_cepstrum_rows(self._h, a.data_ptr(), gg.data_ptr(), n, p1 - 1, int(lim), cep.data_ptr(),
                                      s.cuda_stream))
         return cep
+
+
+def _dev_ptr(t: torch.Tensor, name: str) -> int:
+    """Device address of a device tensor, or of a pinned host tensor through its device mapping (the
+    kernel then stores straight into host memory)."""
+    if t.is_cuda:
+        return t.data_ptr()
+    if t.is_pinned():
+        dp = ctypes.c_void_p()
+        check(lib.fdlp_mapped_ptr(ctypes.c_void_p(t.data_ptr()), ctypes.byref(dp)))
+        return dp.value
+    raise ValueError("%s must be a device tensor or a pinned host tensor" % name)
+
+
+def q_widen(q, decimals: int = 3, threads: int = 1, out: Optional[np.ndarray] = None) -> np.ndarray:
+    """float32 ark values of compact codes (host int16 array or CPU tensor; fdlp_q_widen): bitwise the
+    float32 rows fdlp_compute writes to ``out`` with the same ark_decimals."""
+    qa = np.ascontiguousarray(q.numpy() if isinstance(q, torch.Tensor) else q, dtype=np.int16)
+    if out is None:
+        out = np.empty(qa.shape, dtype=np.float32)
+    elif out.dtype != np.float32 or out.size < qa.size or not out.flags.c_contiguous:
+        raise ValueError("out must be a contiguous float32 array of at least q.size elements")
+    check(lib.fdlp_q_widen(qa.ctypes.data, qa.size, int(decimals), out.ctypes.data, int(threads)))
+    return out
 
 
 def device_checks(reset: bool = False):
