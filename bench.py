@@ -387,9 +387,12 @@ def xfer_child_spec(args, world, rank, local, argv=None, environ=None):
     env = {k: v for k, v in environ.items() if k not in RANK_ENV}
     env["GPU_MAX_HW_QUEUES"] = str(args.xfer_hw_queues)
     if world > 1:
-        vis = environ.get("HIP_VISIBLE_DEVICES")
+        # the rank's GPU among the visible ones: HIP_VISIBLE_DEVICES wins over CUDA_VISIBLE_DEVICES in HIP, so
+        # the list comes from the first that is set, and the child sees only HIP_VISIBLE_DEVICES
+        vis = environ.get("HIP_VISIBLE_DEVICES") or environ.get("CUDA_VISIBLE_DEVICES")
         ids = [v.strip() for v in vis.split(",") if v.strip()] if vis else None
         env["HIP_VISIBLE_DEVICES"] = ids[local % len(ids)] if ids else str(local)
+        env.pop("CUDA_VISIBLE_DEVICES", None)
     return out, env
 
 
@@ -429,16 +432,25 @@ def run_xfer_child(args, world=1, rank=0, local=0):
     return json.loads(lines[-1])["with_transfers"]
 
 
-def host_cores():
+CPU_WORKERS_CAP = 16  # without OMP_NUM_THREADS: one oracle process holds ~1 GB on REVERB-sized utterances
+
+
+def host_cores(with_rule=False):
     """The host cores this process may use: its CPU affinity, capped at the CPU share a pool gives a job
     (OMP_NUM_THREADS, which the GPU pool sets to a one-GPU job's share; os.cpu_count() there counts every
-    CPU of the machine, most of them other jobs')."""
+    CPU of the machine, most of them other jobs'), or at CPU_WORKERS_CAP when OMP_NUM_THREADS is unset.
+    with_rule: also return how the count was chosen (recorded in the cpu_baseline block)."""
     try:
         n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         n = os.cpu_count() or 1
     share = os.environ.get("OMP_NUM_THREADS", "")
-    return max(1, min(n, int(share))) if share.isdigit() and int(share) > 0 else max(1, n)
+    if share.isdigit() and int(share) > 0:
+        v, rule = max(1, min(n, int(share))), "min(affinity %d, OMP_NUM_THREADS %s)" % (n, share)
+    else:
+        v, rule = max(1, min(n, CPU_WORKERS_CAP)), "min(affinity %d, cap %d; OMP_NUM_THREADS unset)" % (
+            n, CPU_WORKERS_CAP)
+    return (v, rule) if with_rule else v
 
 
 def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, audio_s, world, dd, sync, dev, B):
@@ -641,6 +653,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
         per = args.cpu_per_worker or (10 if args.config == "reverb" else 24)
         cpu = cpu_baseline(args.config, [t for _, t, _ in mine], args.cpu_workers, per, noise_host)
+        cpu["workers_rule"] = ("--cpu-workers %d" % args.cpu_workers if args.cpu_workers != host_cores()
+                               else "default: " + host_cores(with_rule=True)[1])
 
     # PCIe-inclusive pass of every rank in a child process (before this process touches the GPU):
     # GPU_MAX_HW_QUEUES is read once per process, and the headline keeps the process default.  The ranks'

@@ -1,8 +1,9 @@
-// Microbenchmark: time of lpc_env_kernel per phase subset on the WSJ shape (327680 items = 4096 frames x 80
-// bands, p = 150, M = 100, 150 envelope samples).  Build one binary per phase mask:
-//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DFDLP_LPC_PHASES=7 -I speech_recognition_tools_amd/csrc \
+// Microbenchmark: time of the LPC stage kernels (launch_lpc_env: Durbin + cepstrum + envelope) alone on the
+// WSJ shape (327680 items = 4096 frames x 80 bands, p = 150, M = 100, 150 envelope samples) or REVERB's M:
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I speech_recognition_tools_amd/csrc \
 //         benchmarks/lpc_env_phases.hip -o benchmarks/lpc_env_p7
-// (mask bits: 1 Durbin, 2 cepstrum, 4 envelope).  r is the autocorrelation of an AR(2) process.
+// r is the autocorrelation of an AR(2) process.  (The round-3/4 per-phase splits of DESIGN.md §6 came from
+// phase masks compiled into the kernel then; the product kernel no longer carries them.)
 #include "../speech_recognition_tools_amd/csrc/fdlp_lpc.hip"
 
 #include <math.h>
@@ -63,6 +64,6 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(env.data(), d_env, env.size() * 8, hipMemcpyDeviceToHost));
   double cs = 0;
   for (double v : env) cs += v;
-  printf("lpc_env phases=%d items=%d M=%d: %.4f ms/launch (checksum %.6e)\n", FDLP_LPC_PHASES, items, M, ms / reps, cs);
+  printf("lpc_env items=%d M=%d: %.4f ms/launch (checksum %.6e)\n", items, M, ms / reps, cs);
   return 0;
 }

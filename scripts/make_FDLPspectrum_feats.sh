@@ -116,13 +116,36 @@ feat_opts="--fbank_type=$fbank_type --gamma_weight=$gamma_weight --add_reverb=$a
 --add_noise=$add_noise --coeff_num=$coeff_num --coeff_range=$coeff_range --order=$order \
 --overlap_fraction=$overlap_fraction --nfilters=$nfilters --fduration=$fduration --frate=$frate"
 
+# the files the options name, whose contents the features depend on (an in-place edit must invalidate a
+# finished JOB): --lifter_config, noises/<type>.wav of --add_noise <type>,<snr> and the RIR of --add_reverb
+# (both relative to the working directory, features.py:34-44, :75-91), and wav.scp + segments when the
+# shards are segment dumps (their scp lines are ark offsets, unchanged by an edit of the audio)
+ref_files=()
+[ -n "$lifter_config" ] && ref_files+=("$lifter_config")
+case $add_noise in clean|diff) ;; *) ref_files+=("noises/${add_noise%%,*}.wav") ;; esac
+case $add_reverb in
+  small_room) ref_files+=(./RIR/RIR_SmallRoom1_near_AnglA.wav) ;;
+  medium_room) ref_files+=(./RIR/RIR_MediumRoom1_far_AnglA.wav) ;;
+  large_room) ref_files+=(./RIR/RIR_LargeRoom1_far_AnglA.wav) ;;
+esac
+[ -f "$segment" ] && ref_files+=("$scp" "$segment")
+ref_sums() { local f; for f in "${ref_files[@]}"; do echo "$f $(cksum < "$f" 2>/dev/null || echo missing)"; done; }
+
 job_key() {  # job_key <n> <shard> <scp-type-opt>: the JOB's identity, written to its key file
   local n=$1 shard=$2 stype=$3
-  { echo "$add_opts $stype $feat_opts compute_cmvn=$compute_cmvn"; cat "$shard"; } | cksum > "$log_dir/resume_${name}.$n.key"
+  { echo "$add_opts $stype $feat_opts compute_cmvn=$compute_cmvn"; ref_sums; cat "$shard"; } | cksum \
+    > "$log_dir/resume_${name}.$n.key"
 }
-job_done() {  # the JOB's last finished run had the same key and its outputs exist
-  local n=$1 out="$feat_dir/melspec_${name}.$1"
-  cmp -s "$log_dir/resume_${name}.$n.key" "$out.done" && [ -f "$out.ark" ] && [ -f "$out.scp" ]
+job_outputs() {  # job_outputs <n>: every output a finished JOB leaves (the .len and CMVN stats when asked for)
+  local out="$feat_dir/melspec_${name}.$1"
+  echo "$out.ark" "$out.scp"
+  $write_utt2num_frames && echo "$out.len"
+  $compute_cmvn && echo "$feat_dir/cmvn_${name}.$1.mat"
+}
+job_done() {  # the JOB's last finished run had the same key and all its outputs exist
+  local n=$1 f
+  cmp -s "$log_dir/resume_${name}.$n.key" "$feat_dir/melspec_${name}.$n.done" || return 1
+  for f in $(job_outputs $n); do [ -f "$f" ] || return 1; done
 }
 
 run_jobs() {  # run_jobs <list-pattern containing JOB> <scp-type-opt>
@@ -145,8 +168,11 @@ run_jobs() {  # run_jobs <list-pattern containing JOB> <scp-type-opt>
     [ "${job_gpu:-0}" != 0 ] && req="$req --gpu $job_gpu"
     # with --resume the launcher still gets the whole JOB array (JOB=a:b is a range); the guard skips
     # the finished JOBs inside it
+    local extra_out=()
+    $write_utt2num_frames && extra_out+=("$feat_dir/melspec_${name}.JOB.len")
+    $compute_cmvn && extra_out+=("$feat_dir/cmvn_${name}.JOB.mat")
     $resume && guard=(bash "$here/scripts/fdlp_resume_guard.sh" "$log_dir/resume_${name}.JOB.key"
-                      "$feat_dir/melspec_${name}.JOB.done" "$feat_dir/melspec_${name}.JOB" --)
+                      "$feat_dir/melspec_${name}.JOB.done" "$feat_dir/melspec_${name}.JOB" "${extra_out[@]}" --)
     $cmd $req JOB=1:$nj "$log_dir/feats_${name}.JOB.log" \
       "${guard[@]}" python3 "$cli" "$pattern" "$feat_dir/melspec_${name}.JOB" $add_opts $cmvn_opt $stype \
         --device_rr=JOB,$ngpu $feat_opts || exit 1

@@ -207,82 +207,58 @@ __device__ __forceinline__ int lslot(int pos, int col) {
 }
 
 // One Stockham stage (radix R, Ns = product of the radices before it) of COLS interleaved length-N
-// columns in LDS; om = the N roots omega_N^q.  IP (in place, in == out): every thread reads and
-// transforms all its butterflies first, then a barrier, then the writes; one buffer instead of two,
-// so twice the workgroups fit a CU's LDS (same arithmetic, bit-identical results).
-template <int N, int COLS, int NT, int Ns, int R, bool SWZ = false, bool IP = false>
-__device__ __forceinline__ void st_stage_c(const double2* __restrict__ in, double2* __restrict__ out,
-                                           const double2* __restrict__ om) {
+// columns in LDS, in place; om = the N roots omega_N^q.  Every thread reads and transforms all its
+// butterflies first, then a barrier, then the writes: one buffer instead of two, so twice the workgroups
+// fit a CU's LDS (round 2: 0.96 -> 0.87 ms for the DCT stage against ping-pong buffers).
+template <int N, int COLS, int NT, int Ns, int R, bool SWZ = false>
+__device__ __forceinline__ void st_stage_c(double2* __restrict__ buf, const double2* __restrict__ om) {
   static_assert(!SWZ || COLS == 8, "swizzle of 8 columns");
   constexpr int NB = N / R, TOT = NB * COLS, ITER = (TOT + NT - 1) / NT, TW0 = N / (Ns * R);
-  const double2* src = in;
-  double2* dst = out;
-  if constexpr (IP) src = out;  // the caller passes the one buffer as out
   auto slot = [&](int pos, int col) { return SWZ ? lslot<SWZ>(pos, col) : pos * COLS + col; };
-  double2 v[IP ? ITER : 1][R];
+  double2 v[ITER][R];
+#pragma unroll
+  for (int it = 0; it < ITER; ++it) {
+    const int b = (int)threadIdx.x + it * NT;
+    if (TOT % NT != 0 && b >= TOT) break;
+    const int col = b % COLS, j = b / COLS;
+    const int k = j % Ns;
+    double2 (&w)[R] = v[it];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const double2 x = buf[slot(j + r * NB, col)];
+      w[r] = (r == 0 || Ns == 1) ? x : cmul(x, om[TW0 * k * r]);
+    }
+    bfly_c<R>(w);
+  }
+  __syncthreads();
 #pragma unroll
   for (int it = 0; it < ITER; ++it) {
     const int b = (int)threadIdx.x + it * NT;
     if (TOT % NT != 0 && b >= TOT) break;
     const int col = b % COLS, j = b / COLS;
     const int k = j % Ns, jq = j / Ns;
-    double2 (&w)[R] = v[IP ? it : 0];
+    const int idxD = jq * Ns * R + k;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const double2 x = src[slot(j + r * NB, col)];
-      w[r] = (r == 0 || Ns == 1) ? x : cmul(x, om[TW0 * k * r]);
-    }
-    bfly_c<R>(w);
-    if constexpr (!IP) {
-      const int idxD = jq * Ns * R + k;
-#pragma unroll
-      for (int r = 0; r < R; ++r) dst[slot(idxD + r * Ns, col)] = w[r];
-    }
-  }
-  if constexpr (IP) {
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-      const int b = (int)threadIdx.x + it * NT;
-      if (TOT % NT != 0 && b >= TOT) break;
-      const int col = b % COLS, j = b / COLS;
-      const int k = j % Ns, jq = j / Ns;
-      const int idxD = jq * Ns * R + k;
-#pragma unroll
-      for (int r = 0; r < R; ++r) dst[slot(idxD + r * Ns, col)] = v[it][r];
-    }
+    for (int r = 0; r < R; ++r) buf[slot(idxD + r * Ns, col)] = v[it][r];
   }
 }
 
-// full length-N DFT of COLS columns, radices R0 R1 ...; returns the buffer holding the result
-// (IP: a only, b unused)
-template <int N, int COLS, int NT, bool SWZ, bool IP, int Ns, int R0, int... Rs>
-__device__ __forceinline__ double2* lds_dft_c(double2* a, double2* b, const double2* om) {
-  if constexpr (IP) {
-    st_stage_c<N, COLS, NT, Ns, R0, SWZ, true>(a, a, om);
-    __syncthreads();
-    if constexpr (sizeof...(Rs) > 0) return lds_dft_c<N, COLS, NT, SWZ, true, Ns * R0, Rs...>(a, b, om);
-    else return a;
-  } else {
-    st_stage_c<N, COLS, NT, Ns, R0, SWZ>(a, b, om);
-    __syncthreads();
-    if constexpr (sizeof...(Rs) > 0) return lds_dft_c<N, COLS, NT, SWZ, false, Ns * R0, Rs...>(b, a, om);
-    else return b;
-  }
+// full length-N DFT of COLS columns in place in `a`, radices R0 R1 ...
+template <int N, int COLS, int NT, bool SWZ, int Ns, int R0, int... Rs>
+__device__ __forceinline__ double2* lds_dft_c(double2* a, const double2* om) {
+  st_stage_c<N, COLS, NT, Ns, R0, SWZ>(a, om);
+  __syncthreads();
+  if constexpr (sizeof...(Rs) > 0) return lds_dft_c<N, COLS, NT, SWZ, Ns * R0, Rs...>(a, om);
+  else return a;
 }
-
-#ifndef FDLP_DCT_IP
-#define FDLP_DCT_IP 1  // in-place Stockham stages in the specialised DCT kernels (0: ping-pong buffers)
-#endif
-constexpr bool kDctIP = FDLP_DCT_IP != 0;
 
 template <int N1>
 struct DctRadices1;
 template <>
 struct DctRadices1<100> {
   template <int COLS, int NT>
-  __device__ static double2* run(double2* a, double2* b, const double2* om) {
-    return lds_dft_c<100, COLS, NT, false, kDctIP, 1, 4, 5, 5>(a, b, om);
+  __device__ static double2* run(double2* a, const double2* om) {
+    return lds_dft_c<100, COLS, NT, false, 1, 4, 5, 5>(a, om);
   }
 };
 template <int N2>
@@ -290,8 +266,8 @@ struct DctRadices2;
 template <>
 struct DctRadices2<120> {
   template <int COLS, int NT, bool SWZ = false>
-  __device__ static double2* run(double2* a, double2* b, const double2* om) {
-    return lds_dft_c<120, COLS, NT, SWZ, kDctIP, 1, 4, 2, 3, 5>(a, b, om);
+  __device__ static double2* run(double2* a, const double2* om) {
+    return lds_dft_c<120, COLS, NT, SWZ, 1, 4, 2, 3, 5>(a, om);
   }
 };
 
@@ -302,7 +278,7 @@ __global__ __launch_bounds__(256) void frames_dft1_c_kernel(DevConsts c, const v
                                                             const double2* __restrict__ om1,
                                                             double2* __restrict__ z, int nframes) {
   constexpr int NT = 256;
-  __shared__ double2 bufA[N1 * COLS], bufB[kDctIP ? 1 : N1 * COLS], oms[N1], twb[N2];
+  __shared__ double2 bufA[N1 * COLS], oms[N1], twb[N2];
   // 1-D grid, XCD-mapped: the column blocks of a frame run on one XCD (their z rows share L2 lines)
   constexpr int NBX = (N2 + COLS - 1) / COLS;
   const int it0 = xcd_item();
@@ -340,7 +316,7 @@ __global__ __launch_bounds__(256) void frames_dft1_c_kernel(DevConsts c, const v
     bufA[n1 * COLS + col] = val;
   }
   __syncthreads();
-  const double2* res = DctRadices1<N1>::template run<COLS, NT>(bufA, bufB, oms);
+  const double2* res = DctRadices1<N1>::template run<COLS, NT>(bufA, oms);
 #pragma unroll
   for (int it = 0; it < (TOT + NT - 1) / NT; ++it) {
     const int e = (int)threadIdx.x + it * NT;
@@ -361,7 +337,7 @@ __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const doub
   // scale2 = 2 / sqrt(2N): dct(.) / np.sqrt(2N) (:178) as one multiplication (within an ulp of the
   // reference's division; no fp64 division per coefficient)
   constexpr int NT = 256, HALF = COLS / 2;
-  __shared__ double2 bufA[N2 * COLS], bufB[kDctIP ? 1 : N2 * COLS], oms[N2];
+  __shared__ double2 bufA[N2 * COLS], oms[N2];
   __shared__ double2 pw1[N1], pw2[N2], rw1[N1], rw2[N2];  // factored twiddles (TWF)
   // 1-D grid, XCD-mapped: the row-pair blocks of a frame run on one XCD, so the 32-B runs they store
   // into each D line (k = k1 + N1 k2: 4 consecutive k1 per block) merge in that XCD's L2
@@ -397,7 +373,7 @@ __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const doub
     bufA[lslot<SWZ>(n2, row)] = v;
   }
   __syncthreads();
-  const double2* res = DctRadices2<N2>::template run<COLS, NT, SWZ>(bufA, bufB, oms);
+  const double2* res = DctRadices2<N2>::template run<COLS, NT, SWZ>(bufA, oms);
   const double2* post = (const double2*)c.post;
   const double2* rtw = (const double2*)c.rtw;
   constexpr int M = N1 * N2;
@@ -449,9 +425,12 @@ __global__ __launch_bounds__(256) void dft2_dct_c_kernel(DevConsts c, const doub
 //    Pass-3 tasks are laid out so the task holding X[M - k] sits in the adjacent lane (lane ^ 1): the
 //    unpack takes it by DPP quad_perm.  No Z intermediate in HBM: the frame is read once and D written
 //    once (the four-step pair above moves Z = 384 KB per frame through HBM).
-//    Persistent workgroups (one per CU, LDS-bound): the tables are staged once, and the next frame's
-//    descriptor and int16 samples are loaded during the current frame's passes 2-3, its window during
-//    the current frame's row writes, so the gather latency (14 of 40 us per frame, r03am) is hidden.
+//    One workgroup per two frames, as straight-line code (frame 2 b, then 2 b + 1): the twiddle and
+//    unpack tables are staged in LDS once for both.  The samples come by the single-bounce reflect fast
+//    gather (int16 PCM straight into registers, noise-mixed frames included, the window pre-permuted into
+//    16-byte pieces, dct1_fast); the diff filter, fp64 input and multi-bounce padding take the LDS-staged
+//    general gather.  (No cross-frame prefetch: a persistent loop or a prefetch of the second frame spills,
+//    see kDctFramesPerBlock.)
 //    The LDS images are padded (exchange 1: k1 stride 601 = 25 mod 32; exchange 2: k2a stride 529) and
 //    the twiddle tables laid out [k1][t mod 16] x [k1][t div 16] and [k2a][q3], so the lanes of an LDS
 //    instruction spread over the banks (benchmarks/dct_lds_model.py).

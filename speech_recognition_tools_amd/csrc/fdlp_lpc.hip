@@ -451,9 +451,6 @@ __device__ __forceinline__ void cep_block_step(int b0, int M, int l, double gg, 
   if constexpr (KK + 1 < 16) cep_block_step<KK + 1>(b0, M, l, gg, inv_n, la, n, acc, mine, amax);
 }
 
-#ifndef FDLP_LPC_PHASES
-#define FDLP_LPC_PHASES 7  // bit 0 Durbin, 1 cepstrum, 2 envelope (benchmarks/lpc_env_phases.hip only)
-#endif
 
 // -----------------------------------------------------------------------------------------
 // Durbin in lattice form with CONTIGUOUS chunks: in phase S (orders k < 16 S) lane l of the row owns
@@ -796,9 +793,9 @@ __host__ __device__ constexpr int c4_item_stride(int SL4) {
   const int need = 4 * SL4;
   return need + ((28 - need % 32) + 32) % 32;
 }
-constexpr int kC4Guard = 24;
+constexpr int kC4Guard = 24;  // doubles below item 0's image (the mirrored B reads reach index -4 kC4Step - 1)
 // the phase that ends at order p holds it: p <= 4 S - 2 = cap - 2
-__device__ __forceinline__ bool k_done_ok(int p, int cap) { return p <= cap - 2; }  // doubles below item 0's image (the mirrored B reads reach index -4 kC4Step - 1)
+__device__ __forceinline__ bool k_done_ok(int p, int cap) { return p <= cap - 2; }
 
 // Orders [k0, min(p, 4 S - 2)] of phase S, then the next phase.  Returns (in cap) 4 S of the phase that
 // ends at order p and leaves its A in img (positions < cap; exactly 0 past p), gg in g.
@@ -1032,7 +1029,7 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
         contig_load_r1<1>(R11, rr, A.nlags, p, l, valid);
         double part = lane0 ? R11[0] : 0.0;  // order 1: b^(0) . R1 = r_1
         double E = r0;
-        if (FDLP_LPC_PHASES & 1) contig_durbin<SL, 1>(A1, B1, R11, part, E, la, rr, A.nlags, p, l, valid, gg, r0);
+        contig_durbin<SL, 1>(A1, B1, R11, part, E, la, rr, A.nlags, p, l, valid, gg, r0);
       }
       // la[0 .. 16 SL) holds a_0 .. a_p (zeros beyond p); zero the rest of the a region
       for (int q = l + 16 * SL; q < NAL; q += 16) la[q] = 0.0;
@@ -1061,7 +1058,7 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
 #pragma unroll
       for (int b = 0; b < CB; ++b) {
         const int b0 = 16 * b;
-        if (b0 >= ((FDLP_LPC_PHASES & 2) ? M : 0)) break;
+        if (b0 >= M) break;
         const int n = b0 + l;
         double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
         if (b > 0) asm volatile("s_nop 1");  // kc[b - 1] was just written: DPP reads need 2 wait states
@@ -1100,7 +1097,7 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
       // only c_0 .. c_{Me-1} reach the envelope (fft(., env_nfft) truncates, :201); all M are computed
       // when the cepstra themselves are an output (debug / modulation-spectrum mode)
       const int Mc = A.cep_out ? M : A.Me;
-      const int NB = (FDLP_LPC_PHASES & 2) ? (Mc + 15) >> 4 : 0;
+      const int NB = (Mc + 15) >> 4;
       // the lane's LDS byte address la + l + 1: V_q[j] = la[16 (q+1) + l - j] at byte offset 8 (16 q + 15 - j)
       const uint32_t aaddr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) double*)(la + l + 1));
       for (int sb = 0; sb < NB; sb += R) {
@@ -1136,7 +1133,7 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
       }
       wave_lds_sync();
     }
-    for (int b0 = 0; b0 < ((CB == 0 && (FDLP_LPC_PHASES & 2)) ? M : 0); b0 += 16) {
+    for (int b0 = 0; b0 < (CB == 0 ? M : 0); b0 += 16) {
       const int n = b0 + l;
       const double inv_n = 1.0 / (double)(n > 0 ? n : 1);
       // finished blocks: four independent FMA chains (the trip count is uniform across the wave)
@@ -1193,7 +1190,7 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
     wave_lds_sync();
     if constexpr (CB < 0) {
       if (A.env_nfft == 300 && A.Me == 300 && A.kk == 150) {  // the recipes' REVERB envelope: FFT route
-        if (FDLP_LPC_PHASES & 4) env_fft300(cw, A.env_cos, A.env_win, A.env + (int64_t)(valid ? item : 0) * A.kk, l, valid);
+        env_fft300(cw, A.env_cos, A.env_win, A.env + (int64_t)(valid ? item : 0) * A.kk, l, valid);
         continue;
       }
     }
@@ -1217,7 +1214,7 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
       if (16 * (q0 + kEnvChunk) <= A.env_nfft) setup(std::true_type{});
       else setup(std::false_type{});
       int n = 1;
-      for (; n + 1 < ((FDLP_LPC_PHASES & 4) ? A.Me : 0); n += 2) {
+      for (; n + 1 < A.Me; n += 2) {
         const double wo = cw[n], we = cw[n + 1];
 #pragma unroll
         for (int q = 0; q < kEnvChunk; ++q) {
@@ -1262,7 +1259,7 @@ __global__ __launch_bounds__(64) void lpc_env_kernel(LpcEnvArgs A) {
   for (int q = l; q < nlags; q += 16) lr[q] = valid ? A.r[(int64_t)item * nlags + q] : 1.0;
   for (int q = l; q < NAL; q += 16) la[q] = q == 0 ? 1.0 : 0.0;
   wave_lds_sync();
-  const double gg = (FDLP_LPC_PHASES & 1) ? durbin16(la, lr, p, l) : lr[0];
+  const double gg = durbin16(la, lr, p, l);
   if (valid && A.a_out) {
     for (int i = l; i <= p; i += 16) A.a_out[(int64_t)item * (p + 1) + i] = la[i];
     if (l == 0) A.gg_out[item] = gg;
@@ -1272,7 +1269,7 @@ __global__ __launch_bounds__(64) void lpc_env_kernel(LpcEnvArgs A) {
   // blocks of 16 coefficients: the finished blocks enter as a lane-parallel dot product, the block
   // itself as a 16-step recurrence with the new c_k broadcast along the row.
   double* cs = lr;
-  for (int b0 = 0; b0 < ((FDLP_LPC_PHASES & 2) ? M : 0); b0 += 16) {
+  for (int b0 = 0; b0 < M; b0 += 16) {
     const int n = b0 + l;
     const double inv_n = 1.0 / (double)(n > 0 ? n : 1);
     double acc = 0.0;
@@ -1317,7 +1314,7 @@ __global__ __launch_bounds__(64) void lpc_env_kernel(LpcEnvArgs A) {
     c2[q] = 2.0 * c1;
   }
   int n = 1;
-  for (; n + 1 < ((FDLP_LPC_PHASES & 4) ? A.Me : 0); n += 2) {
+  for (; n + 1 < A.Me; n += 2) {
     const double wo = cw[n], we = cw[n + 1];
 #pragma unroll
     for (int q = 0; q < TS; ++q) {

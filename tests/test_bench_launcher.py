@@ -71,3 +71,36 @@ def test_pcie_children_combine():
     x = b.combine_xfer_children(got)
     assert abs(x["value"] - 16.0) < 1e-12 and x["ms_per_step"] == 12.5 and x["per_rank_value"] == [10.0, 8.0]
     assert b.combine_xfer_children([got[0], None]) is None
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod2", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+@pytest.mark.parametrize("environ,local,want", [
+    ({"HIP_VISIBLE_DEVICES": "4,5,6,7"}, 1, "5"),
+    ({"CUDA_VISIBLE_DEVICES": "2,3"}, 1, "3"),                              # a pool that sets only CUDA_*
+    ({"HIP_VISIBLE_DEVICES": "6,7", "CUDA_VISIBLE_DEVICES": "0,1"}, 0, "6"),  # HIP's list wins, as in HIP
+    ({}, 3, "3"),
+])
+def test_pcie_child_lands_on_the_ranks_gpu(environ, local, want):
+    """The child of rank `local` sees exactly the rank's physical GPU through HIP_VISIBLE_DEVICES, whichever
+    of HIP_/CUDA_VISIBLE_DEVICES the pool set, and no CUDA_VISIBLE_DEVICES that HIP could re-index."""
+    b = _bench_module()
+    args = b.parse_args(["--gpus", "4"])
+    _, env = b.xfer_child_spec(args, 4, local, local, argv=["--gpus", "4"], environ=environ)
+    assert env["HIP_VISIBLE_DEVICES"] == want and "CUDA_VISIBLE_DEVICES" not in env
+
+
+def test_cpu_workers_default_is_capped(monkeypatch):
+    b = _bench_module()
+    monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
+    n, rule = b.host_cores(with_rule=True)
+    assert 1 <= n <= b.CPU_WORKERS_CAP and "unset" in rule
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    n, rule = b.host_cores(with_rule=True)
+    assert n == min(3, len(os.sched_getaffinity(0))) and "OMP_NUM_THREADS 3" in rule

@@ -188,6 +188,20 @@ def test_driver_resume_skips_finished_jobs(tmp_path):
     assert run("--resume", "true", "--order", "40") == [1, 2, 3]  # other options: new keys
     assert run("--resume", "true", "--order", "40") == []
     assert run() == [1, 2, 3]
+    (fbank / "melspec_dev.3.len").unlink()  # --write_utt2num_frames: the .len is an output too
+    assert run("--resume", "true") == [3]
+
+
+def test_driver_resume_sees_edits_of_the_files_the_options_name(tmp_path):
+    """The resume key hashes the contents of the files the options name: an in-place edit
+    of the --lifter_config file reruns every JOB with the same option string."""
+    run, fbank = _resume_setup(tmp_path)
+    lif = tmp_path / "lifter.txt"
+    lif.write_text("1.0 " * 100 + "\n")
+    assert run("--lifter_config", str(lif)) == [1, 2, 3]
+    assert run("--resume", "true", "--lifter_config", str(lif)) == []
+    lif.write_text("0.5 " * 100 + "\n")
+    assert run("--resume", "true", "--lifter_config", str(lif)) == [1, 2, 3]
 
 
 def test_driver_resume_with_launcher_wraps_jobs_in_the_guard(tmp_path):
@@ -231,3 +245,13 @@ def test_resume_guard(tmp_path):
     assert go("touch", str(mark)) == (0, False)  # up to date: skipped
     key.write_text("3 4\n")
     assert go("touch", str(mark)) == (0, True) and stamp.read_text() == "3 4\n"
+    # extra outputs before the "--" (.len, CMVN stats): all must exist for a skip
+    extra = tmp_path / "o.len"
+    r = subprocess.run(["bash", guard, str(key), str(stamp), str(out), str(extra), "--", "touch", str(mark)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and mark.exists()
+    mark.unlink()
+    extra.write_text("")
+    r = subprocess.run(["bash", guard, str(key), str(stamp), str(out), str(extra), "--", "touch", str(mark)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and not mark.exists()

@@ -272,12 +272,49 @@ def test_lattice_durbin_matches_lds_durbin(name, monkeypatch):
         assert np.abs(a[fin] - b[fin]).max() <= TOL_UTT.get(u, 1e-6), (name, u)
 
 
+def durbin_errors(plans, nf):
+    """Per-item errors of each plan's Durbin against scipy's solve_toeplitz on the same r (the oracle,
+    features.py:226-228): a as max |a - a_ref| / max |a_ref|, gg as |gg - gg_ref| / gg_ref, over the items
+    with r_0 > 0."""
+    from oracle import fdlp_oracle as O
+    d = [pl.debug_fetch(nf, keys=("r", "a", "gg")) for pl in plans]
+    r = d[0]["r"].reshape(-1, d[0]["r"].shape[-1])
+    p = d[0]["a"].shape[-1] - 1
+    live = np.flatnonzero(r[:, 0] > 0)
+    ea = np.empty((len(plans), live.size))
+    eg = np.empty((len(plans), live.size))
+    for n, i in enumerate(live):
+        a_ref, gg_ref = O.lpc_from_autocorr(r[i], p)
+        sc = np.abs(a_ref).max()
+        for k, dk in enumerate(d):
+            ea[k, n] = np.abs(dk["a"].reshape(-1, p + 1)[i] - a_ref).max() / sc
+            eg[k, n] = abs(dk["gg"].reshape(-1)[i] - gg_ref) / abs(gg_ref)
+    return ea, eg
+
+
+def assert_durbin4_accuracy(ea4, ea8, eg4, eg8, what):
+    """durbin4 (the default) at least as accurate as durbin8 (the kernel it replaced) against solve_toeplitz.
+    The two differ only in rounding (the order-k dot products summed over 4 lanes x 1 chain instead of 8
+    lanes x 4 chains), which Levinson amplifies by each item's conditioning, so per item either kernel can
+    be the more accurate one by a random factor: over the golden sets and orders 128-150 the ratio e4 / e8
+    has median 0.81-0.83, p99 3.8-4.6 and maximum 6.3-10.2, and 6-7.5 % of the items exceed 2
+    (tests/data/durbin4_accuracy_r05c.jsonl, benchmarks/durbin4_accuracy.py).  So the bars are on the
+    distribution -- median, p99 and worst item no worse than durbin8's -- plus a per-item bound of 16x
+    durbin8's error (above the measured maximum) or 1e-9, and gg within 1e-11 of the oracle's gain."""
+    for q in (0.5, 0.99, 1.0):
+        assert np.quantile(ea4, q) <= max(1e-13, 1.25 * np.quantile(ea8, q)), (what, q, np.quantile(ea4, q),
+                                                                             np.quantile(ea8, q))
+    assert np.all(ea4 <= np.maximum(1e-9, 16 * ea8)), (what, float((ea4 / np.maximum(ea8, 1e-300)).max()))
+    assert eg4.max() <= 1e-11 and eg8.max() <= 1e-11, (what, float(eg4.max()), float(eg8.max()))
+
+
 @pytest.mark.parametrize("name", ["wsj", "reverb", "mel80"])
 def test_durbin4_matches_durbin8(name):
     """durbin4_kernel (4 lanes per item, the default for 128 <= p <= 150) against durbin8_kernel (8 lanes,
-    FDLP_LPC_LATTICE8): the same lattice recursion with the order-k dot products summed over 4 lanes x 2
-    chains instead of 8 lanes x 4 chains.  Features within 1e-6 (the ill-conditioned short2 / PESQ bands
-    as for the LDS cross-check), and a / gg of every item of a full batch at 1e-6 / 1e-9 relative."""
+    FDLP_LPC_LATTICE8): the same lattice recursion with the order-k dot products summed over 4 lanes x 1
+    chain instead of 8 lanes x 4 chains.  Features within 1e-6 (the ill-conditioned short2 / PESQ bands
+    as for the LDS cross-check), gg of every item within 1e-9 of durbin8's, and a / gg of every item as
+    accurate against solve_toeplitz as durbin8's (assert_durbin4_accuracy)."""
     meta, sig, ref, z = load_golden(name)
     p4, res4 = run_gpu(meta, sig, z, debug=True)
     p8, res8 = run_gpu(meta, sig, z, debug=True, lpc="lattice8")
@@ -287,25 +324,38 @@ def test_durbin4_matches_durbin8(name):
         np.testing.assert_array_equal(np.isfinite(a), fin)
         assert np.abs(a[fin] - b[fin]).max() <= TOL_UTT.get(u, 1e-6), (name, u)
         assert np.abs(a - ref[u]).max() <= TOL_UTT.get(u, TOL), (name, u)
-    # a of every item against scipy's solve_toeplitz on the same r (the oracle, features.py:226): the two
-    # Durbin kernels differ only in rounding, which Levinson amplifies by the system's conditioning (the
-    # empty 4-8 kHz bands of the upsampled PESQ clips, short2), so durbin4 must be as accurate as durbin8
-    # item by item (within 10x or 1e-7 relative) and at least as accurate in the median
-    from oracle import fdlp_oracle as O
     nf = sum(p4.geometry(sig[u].size)[0] for u in meta["utts"])
-    d4, d8 = p4.debug_fetch(nf, keys=("r", "a", "gg")), p8.debug_fetch(nf, keys=("a", "gg"))
-    r = d4["r"].reshape(-1, d4["r"].shape[-1])
-    a4, a8 = d4["a"].reshape(-1, d4["a"].shape[-1]), d8["a"].reshape(-1, d8["a"].shape[-1])
-    p = a4.shape[1] - 1
-    live = np.flatnonzero(r[:, 0] > 0)
-    assert live.size >= 80
-    e4, e8 = np.empty(live.size), np.empty(live.size)
-    for n, i in enumerate(live):
-        a_ref, _ = O.lpc_from_autocorr(r[i], p)
-        sc = np.abs(a_ref).max()
-        e4[n], e8[n] = np.abs(a4[i] - a_ref).max() / sc, np.abs(a8[i] - a_ref).max() / sc
-    assert np.all(e4 <= np.maximum(1e-7, 10 * e8)), (name, float(e4.max()), float(e8.max()))
-    assert np.median(e4) <= max(1e-12, 2 * np.median(e8)), (name, float(np.median(e4)), float(np.median(e8)))
+    g4 = p4.debug_fetch(nf, keys=("gg",))["gg"].reshape(-1)
+    g8 = p8.debug_fetch(nf, keys=("gg",))["gg"].reshape(-1)
+    live = g8 > 0
+    assert live.sum() >= 80
+    np.testing.assert_allclose(g4[live], g8[live], rtol=1e-9, atol=0)  # gg feeds c0 = log(sqrt(gg))
+    (e4, e8), (eg4, eg8) = durbin_errors([p4, p8], nf)
+    assert_durbin4_accuracy(e4, e8, eg4, eg8, name)
+
+
+@pytest.mark.parametrize("order", [128, 130, 146, 149])
+def test_durbin4_orders_below_150(order):
+    """durbin4_kernel at the orders where it stops at an earlier phase than at the recipes' 150 (the per-item
+    copy of a row shorter than its capacity, and the zero margins the select-free relayout relies on:
+    ADVICE round 4): WSJ golden signals with --order changed, against the oracle at TOL (the jitter of
+    O.compute_utterances), against durbin8_kernel and the LDS Durbin within 1e-6 (short2 3e-3), and a / gg
+    per item against solve_toeplitz as for p = 150."""
+    from oracle import fdlp_oracle as O
+    meta, sig, ref, z = load_golden("wsj")
+    meta = dict(meta, opts=dict(meta["opts"], order=order), seed=5)
+    runs = {k: run_gpu(meta, sig, z, debug=True, lpc=k) for k in ("auto", "lattice8", "lds")}
+    oref = O.compute_utterances(oracle_cfg(meta), {u: sig[u] for u in meta["utts"]}, 5)
+    for u in meta["utts"]:
+        got = runs["auto"][1][u][0]
+        assert got.shape == oref[u].shape, u
+        assert np.abs(got - oref[u]).max() <= TOL_UTT.get(u, TOL), (order, u, np.abs(got - oref[u]).max())
+        for k in ("lattice8", "lds"):
+            other = runs[k][1][u][0]
+            assert np.abs(got - other).max() <= TOL_UTT.get(u, 1e-6), (order, k, u)
+    nf = sum(runs["auto"][0].geometry(sig[u].size)[0] for u in meta["utts"])
+    (e4, e8), (eg4, eg8) = durbin_errors([runs["auto"][0], runs["lattice8"][0]], nf)
+    assert_durbin4_accuracy(e4, e8, eg4, eg8, order)
 
 
 def test_reverb_kernel_vs_oracle():
