@@ -225,7 +225,7 @@ STAGE_KERNELS = {"dct": ("fdlp::dct_frame", "fdlp::frames_dft1", "fdlp::dft2_dct
                               "structured_mfma": ("fdlp::ac_sweep_kernel", "fdlp::ac_band_kernel"),
                               "direct": ("fdlp::autocorr_kernel",)},
                  "lpc_env": ("fdlp::durbin4_kernel", "fdlp::durbin8_kernel", "fdlp::lpc_env_lattice_kernel", "fdlp::cep_kernel",
-                             "fdlp::env_gemm_kernel"),
+                             "fdlp::env_gemm_kernel", "fdlp::ola_fixup"),
                  "ola_log": ("fdlp::ola_log",)}
 
 
@@ -598,6 +598,8 @@ def parse_args(argv=None):
     ap.add_argument("--pipeline", type=int, default=None, help="sub-batches over two streams (plan default 1)")
     ap.add_argument("--dct-path", default="auto", choices=["auto", "four_step"],
                     help="DCT stage: auto (one dct_frame_kernel per frame at N = 24000) or the four-step pair")
+    ap.add_argument("--ola-path", default="auto", choices=["auto", "separate", "fused"],
+                    help="OLA + log stage (A/B): auto = separate (ola_log_tiled_kernel); fused = inside the LPC kernel")
     ap.add_argument("--lpc-path", default="auto", choices=["auto", "lattice8", "lds"],
                     help="Durbin kernel (A/B): auto = durbin4_kernel for the recipes' p = 150")
     ap.add_argument("--inflight", type=int, default=4,
@@ -737,6 +739,7 @@ def main():
     for pl in plans:
         pl.set_dct_path(args.dct_path)
         pl.set_lpc_path(args.lpc_path)
+        pl.set_ola_path(args.ola_path)
     shifts = [7919 * b for b in range(B)]
     pcms = [pcm] + [torch.roll(pcm, shifts[b]) for b in range(1, B)]
     outs = [out] + [torch.empty_like(out) for _ in range(B - 1)]

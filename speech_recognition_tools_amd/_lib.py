@@ -137,6 +137,8 @@ SIGNATURES = {
     "fdlp_set_dct_path": (c_i32, [c_p, c_i32]),
     "fdlp_dct_path": (c_i32, [c_p]),
     "fdlp_set_pipeline": (c_i32, [c_p, c_i32]),
+    "fdlp_set_ola_path": (c_i32, [c_p, c_i32]),
+    "fdlp_ola_path": (c_i32, [c_p]),
     "fdlp_stage_times": (c_i32, [c_p, P_dbl, P_i32]),
     "fdlp_plan_setup_times": (c_i32, [c_p, P_dbl]),
     "fdlp_dct_rows": (c_i32, [c_p, c_p, c_i32, c_p, c_p]),

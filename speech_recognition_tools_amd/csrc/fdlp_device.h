@@ -109,7 +109,6 @@ constexpr int kDftCols = 8;     // columns (rows) per workgroup in the two DFT p
 // Workgroup b is dispatched to XCD b % 8.  Giving every XCD a contiguous run of work items keeps
 // the items that read the same frame (its D row) on one L2 instead of pulling the row into all
 // eight.  Grid = 8 * ceil(total / 8); the padding workgroups get an index >= total.
-constexpr int kXcds = 8;
 __device__ __forceinline__ int xcd_item() {
   const int per = gridDim.x / kXcds;
   return (int)(blockIdx.x % kXcds) * per + (int)(blockIdx.x / kXcds);
@@ -294,6 +293,19 @@ __device__ __forceinline__ int16_t q_code(double k, bool& bad) {
   if (k >= -32767.0 && k <= 32767.0) return (k == 0.0 && signbit(k)) ? kQNegZero : (int16_t)(int)k;
   bad = true;  // out of range or NaN
   return kQNegZero;
+}
+
+// One feature of the OLA output (computeFDLPSpectrogram.py:227-229): log(clip(acc, 1e-14)) keeping NaN,
+// stored as fp64 (debug), float32 ('%.<d>f'-rounded when decimals >= 0) and / or compact code; the OLA
+// kernel, the fused OLA of the lattice kernel and the boundary fixup all store through this.
+__device__ __forceinline__ void ola_store_feature(double acc, int64_t o, float* __restrict__ out,
+                                                  double* __restrict__ out64, int16_t* __restrict__ outq,
+                                                  int decimals, double scale10, bool& bad) {
+  const double v = log(acc < 1e-14 ? 1e-14 : acc);  // np.clip(a_min=1e-14) keeps NaN; :227
+  if (out64) out64[o] = v;
+  const double k = nearbyint(v * scale10);
+  if (out) out[o] = decimals >= 0 ? (float)(k / scale10) : (float)v;
+  if (outq) outq[o] = q_code(k, bad);
 }
 
 // numpy 'reflect' padding index (getFrames, features.py:146)

@@ -9,6 +9,7 @@
 namespace fdlp {
 
 constexpr int kMaxRadices = 16;
+constexpr int kXcds = 8;  // XCDs of an MI355X; workgroup b is dispatched to XCD b mod 8
 
 // A length-n complex DFT factored into radices (Stockham autosort, one LDS-resident pass).
 struct DftPlan {
@@ -34,6 +35,22 @@ struct UttDesc {
   int32_t L;           // output frames
   int32_t frame0;      // first analysis frame (global index in the batch)
   int32_t F;           // analysis frames
+  int32_t pad;
+};
+
+// Fused OLA + log (lpc_env_lattice_kernel<..., OLA = true>): one chunk = consecutive frames of one utterance
+// that a wave runs in order for one band quad (4 bands), carrying each frame's tail (the rows the next frame
+// also covers) to the next.  Long utterances are cut into chunks between two middle frames (full kk, src 0);
+// such a boundary's overlap rows are finished by ola_fixup_kernel from the two partial sums.
+struct OlaChunk {
+  int32_t frame0;   // first analysis frame (batch index)
+  int32_t nf;       // frames
+  int32_t bin;      // boundary whose second half this chunk's first frame writes (fa), -1: none
+  int32_t bout;     // boundary whose first half this chunk's last frame writes (fb), -1: none
+};
+struct OlaBound {
+  int64_t row0;     // absolute output row of the second frame's dst
+  int32_t len;      // overlap rows (first frame's dst + kk - second frame's dst)
   int32_t pad;
 };
 
@@ -142,9 +159,29 @@ hipError_t launch_cepstrum(int p, int M, const double* a, const double* gg, int 
                            double* cep, hipStream_t s);
 // a_ws / gg_ws: [items, c.lpc_astride] / [items] workspace of the split Durbin (durbin8_kernel,
 // c.lpc_split); a_out / gg_out (debug, [items, p+1] / [items]) get copies
+// Output side of the fused OLA (computeFDLPSpectrogram.py:207-229 inside the lattice kernel); null: the
+// envelopes go to `env` and ola_log_tiled_kernel runs after
+struct OlaFused {
+  const FrameDesc* frames;
+  const UttDesc* utts;
+  const OlaChunk* chunks;   // sorted by nf, longest first
+  const OlaBound* bounds;
+  int nchunks, nbounds;
+  int* counter;             // [8] per-XCD work counters, zeroed on the stream before the launch
+  double* ring;             // [grid, 2, 4, kk] per-wave tails
+  double* fa;               // [nbounds, B, kk] second frame's overlap values
+  double* fb;               // [nbounds, B, kk] first frame's overlap values
+  float* out;
+  double* out64;
+  int16_t* outq;
+  uint32_t* qflag;
+  int decimals;
+};
 hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int items, double* env,
                           double* a_out, double* gg_out, double* cep_out, double* a_ws, double* gg_ws,
-                          hipStream_t s);
+                          hipStream_t s, const OlaFused* ola = nullptr);
+// true when launch_lpc_env can fuse the OLA for this plan (the lattice kernels run)
+bool lpc_env_can_fuse(const DevConsts& c);
 int lpc_env_region(int p, int M);
 // Per-plan launch setup of launch_lpc_env for the current device: sets the kernel's large-LDS
 // attribute and stores the resident block count in c.lpc_blocks.

@@ -21,12 +21,15 @@ namespace fdlp {
 // NaN, float32 (optionally '%.3f'-rounded) row-major stores and the fp64 debug copy.
 // -----------------------------------------------------------------------------------------
 constexpr int kOlaRows = 32;
+constexpr int kOlaFr = 3;   // frames on a tile summed in registers (kk <= 2 hops + 31 rows: every recipe)
+constexpr int kOlaJ = 10;   // bands per thread in that path (B <= 80)
 __global__ __launch_bounds__(256) void ola_log_tiled_kernel(DevConsts c, const double* __restrict__ env,
                                                             const FrameDesc* __restrict__ frames,
                                                             const UttDesc* __restrict__ utts, float* __restrict__ out,
                                                             double* __restrict__ out64, int16_t* __restrict__ outq,
                                                             uint32_t* __restrict__ qflag, int decimals, double scale10) {
   extern __shared__ double tile[];  // [kOlaRows][B + 1]
+  __shared__ int fr_lo, fr_hi;      // the frames overlapping the tile
   const int u = blockIdx.y;
   const UttDesc U = utts[u];
   const int t0 = blockIdx.x * kOlaRows;
@@ -35,17 +38,54 @@ __global__ __launch_bounds__(256) void ola_log_tiled_kernel(DevConsts c, const d
   const int B = c.B, BS = c.B + 1, kk = c.kk;
   const int tid = threadIdx.x;
   for (int q = tid; q < kOlaRows * BS; q += blockDim.x) tile[q] = 0.0;
-  // frames overlapping [t0, t0 + nt): dst is non-decreasing in k; the last one with dst < t0 + nt,
-  // then down while a frame still reaches t0
-  int lo = 0, hi = U.F - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (frames[U.frame0 + mid].dst < t0 + nt) lo = mid; else hi = mid - 1;
+  // frames overlapping [t0, t0 + nt): dst is non-decreasing in k, so they are a range; every thread tests
+  // its own frames at once (one memory round trip, not a binary search of dependent loads) and the range
+  // ends are the smallest / largest frame that overlaps (a frame past t0 + nt or ending before t0 does not)
+  if (tid == 0) {
+    fr_lo = U.F;
+    fr_hi = -1;
   }
-  int kf = lo;
-  while (kf > 0 && frames[U.frame0 + kf - 1].dst + kk > t0) --kf;
   __syncthreads();
+  for (int k = tid; k < U.F; k += blockDim.x) {
+    const FrameDesc fd = frames[U.frame0 + k];
+    if (fd.dst < t0 + nt && fd.dst + kk > t0) {
+      atomicMin(&fr_lo, k);
+      atomicMax(&fr_hi, k);
+    }
+  }
+  __syncthreads();
+  const int kf = fr_lo, lo = fr_hi;
   const int tt = tid % kOlaRows, jj = tid / kOlaRows;  // 8 band lanes x 32 rows
+  // the cell (tt, j) of the tile belongs to one thread across the frames, so the usual case -- at most
+  // kOlaFr frames on the tile, B <= 8 kOlaJ -- sums in registers with all envelope loads issued before the
+  // first add (one exposed memory latency), in frame order, 0 + e_a + e_b as the reference's in-place adds
+  if (lo - kf < kOlaFr && B <= 8 * kOlaJ) {
+    const int t = t0 + tt;
+    double v[kOlaFr][kOlaJ];
+    bool cov[kOlaFr];
+#pragma unroll
+    for (int m = 0; m < kOlaFr; ++m) {
+      const int k = min(kf + m, U.F - 1);
+      const FrameDesc fd = frames[U.frame0 + k];
+      cov[m] = kf + m <= lo && t < t0 + nt && t >= fd.dst && t < fd.dst + fd.cnt;
+      const double* er = env + (int64_t)(U.frame0 + k) * B * kk + (cov[m] ? fd.src + (t - fd.dst) : 0);
+#pragma unroll
+      for (int i = 0; i < kOlaJ; ++i) {
+        const int j = jj + 8 * i;
+        v[m][i] = cov[m] && j < B ? er[(int64_t)j * kk] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kOlaJ; ++i) {
+      const int j = jj + 8 * i;
+      double acc = 0.0;
+#pragma unroll
+      for (int m = 0; m < kOlaFr; ++m)
+        if (cov[m]) acc = acc + v[m][i];
+      if (j < B) tile[tt * BS + j] = acc;
+    }
+    __syncthreads();
+  } else {
   for (int k = kf; k <= lo; ++k) {
     const FrameDesc fd = frames[U.frame0 + k];
     const int t = t0 + tt;
@@ -56,6 +96,7 @@ __global__ __launch_bounds__(256) void ola_log_tiled_kernel(DevConsts c, const d
     }
     __syncthreads();
   }
+  }
   // t = q / B by a float reciprocal: (q + 0.5) / B sits at least 0.5 / B from an integer, and two float
   // roundings move it by at most (q / B) 2^-22 <= kOlaRows 2^-22, far less for any B below 65536
   const float invB = 1.0f / (float)B;
@@ -63,13 +104,8 @@ __global__ __launch_bounds__(256) void ola_log_tiled_kernel(DevConsts c, const d
   for (int q = tid; q < nt * B; q += blockDim.x) {
     const int t = (int)(((float)q + 0.5f) * invB), j = q - t * B;
     FDLP_CHECK(t >= 0 && t < nt && j >= 0 && j < B);
-    const double acc = tile[t * BS + j];
-    const double v = log(acc < 1e-14 ? 1e-14 : acc);  // np.clip(a_min=1e-14) keeps NaN; :227
-    const int64_t o = (U.out_row + t0 + t) * (int64_t)B + j;
-    if (out64) out64[o] = v;
-    const double k = nearbyint(v * scale10);
-    if (out) out[o] = decimals >= 0 ? (float)(k / scale10) : (float)v;
-    if (outq) outq[o] = q_code(k, bad);
+    ola_store_feature(tile[t * BS + j], (U.out_row + t0 + t) * (int64_t)B + j, out, out64, outq, decimals, scale10,
+                      bad);
   }
   if (bad) *qflag = 1u;
 }

@@ -398,6 +398,17 @@ struct fdlp_plan {
   hipEvent_t staging_done = nullptr;
   bool staging_pending = false;
   int last_frames = 0;
+  // fused OLA (fdlp_set_ola_path; lpc_env_lattice_kernel<..., OLA>): chunk / boundary tables (pinned staging
+  // + device), the work counter, the per-wave tail ring, the boundary halves (grown on demand)
+  int ola_path = FDLP_OLA_AUTO;
+  int ola_last = 0;                  // the OLA the last fdlp_compute ran (FDLP_OLA_FUSED / _SEPARATE)
+  bool env_valid = false;            // ws.env holds the last batch's envelopes (fdlp_debug_fetch)
+  fdlp::OlaChunk *h_chunks = nullptr, *d_chunks = nullptr;
+  fdlp::OlaBound *h_bounds = nullptr, *d_bounds = nullptr;
+  int* d_ola_counter = nullptr;
+  double* d_ola_ring = nullptr;
+  double* d_ola_fab = nullptr;       // fa then fb, [2][cap][B][kk]
+  size_t ola_fab_cap = 0;            // boundaries
   // optional per-stage HIP-event timing (fdlp_set_profiling / fdlp_stage_times)
   bool profiling = false;
   bool debug_intermediates = false;  // keep a/gg/cep of the fused LPC kernel for fdlp_debug_fetch
@@ -460,11 +471,13 @@ int free_plan(fdlp_plan* p) {
                   p->d_om1, p->d_om2, p->d_dct1, p->d_lo, p->d_hi, p->ws.z, p->ws.dct, p->ws.r, p->ws.a, p->ws.gg,
                   p->ws.cep, p->ws.env, p->ws.a_pad, p->d_frames, p->d_utts, p->d_sk_e, p->r_up, p->d_sk_snap,
                   p->d_sk_reg, p->d_faxis, p->r_flat, p->d_fl_ev, p->r_flat_part, p->d_fl_band, p->d_sk_wrap,
-                  p->r_wrap};
+                  p->r_wrap, p->d_chunks, p->d_bounds, p->d_ola_counter, p->d_ola_ring, p->d_ola_fab};
   for (void* d : devs)
     if (d) (void)hipFree(d);
   if (p->h_frames) (void)hipHostFree(p->h_frames);
   if (p->h_utts) (void)hipHostFree(p->h_utts);
+  if (p->h_chunks) (void)hipHostFree(p->h_chunks);
+  if (p->h_bounds) (void)hipHostFree(p->h_bounds);
   if (p->staging_done) (void)hipEventDestroy(p->staging_done);
   if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
   if (p->ev_join) (void)hipEventDestroy(p->ev_join);
@@ -525,6 +538,55 @@ int ola_table(const fdlp_plan* p, int F, int L, const uint8_t* jit, int32_t* dst
     else ptr = ptr + p->ola_hop + (jit ? jit[i - 1] : 0);
   }
   return FDLP_OK;
+}
+
+// Fused OLA tables of a batch (lpc_env_lattice_kernel<..., OLA>, fdlp_internal.h OlaChunk): one chunk per
+// utterance, cut every kOlaChunk frames between two middle frames (full kk, src 0, overlapping) while at least
+// three frames remain, so no chunk runs much longer than the others; chunks sorted longest first for the work
+// counter.  Returns false (the separate OLA kernel runs) when a row would be covered by more than two frames
+// (the fused sum keeps only the previous frame's tail) or the tables do not fit.
+constexpr int kOlaChunk = 8;
+bool build_ola_chunks(fdlp_plan* p, int n_utt, int* nchunks, int* nbounds) {
+  const fdlp::FrameDesc* fr = p->h_frames;
+  const int kk = p->kk;
+  std::vector<fdlp::OlaChunk> ch;
+  int nb = 0;
+  for (int u = 0; u < n_utt; ++u) {
+    const fdlp::UttDesc& U = p->h_utts[u];
+    const fdlp::FrameDesc* f = fr + U.frame0;
+    if (U.F > 0 && f[0].dst != 0) return false;
+    for (int k = 1; k + 1 < U.F; ++k)  // frame k + 1 starts where frame k - 1 ends or later
+      if (f[k + 1].dst < f[k - 1].dst + f[k - 1].cnt) return false;
+    int k0 = 0;
+    int bin = -1;
+    while (k0 < U.F) {
+      int k1 = U.F;  // chunk [k0, k1)
+      int bout = -1;
+      for (int kb = k0 + kOlaChunk; kb + 3 <= U.F; ++kb) {  // the first valid cut at or after k0 + kOlaChunk
+        const fdlp::FrameDesc &a = f[kb - 1], &b = f[kb];
+        const int len = a.dst + kk - b.dst;
+        if (a.cnt == kk && b.cnt == kk && a.src == 0 && b.src == 0 && len > 0 && len <= kk && kb - 1 >= 1) {
+          if (nb >= p->max_frames) return false;
+          fdlp::OlaBound& bd = p->h_bounds[nb];
+          bd.row0 = U.out_row + b.dst;
+          bd.len = len;
+          bd.pad = 0;
+          bout = nb++;
+          k1 = kb;
+          break;
+        }
+      }
+      ch.push_back(fdlp::OlaChunk{U.frame0 + k0, k1 - k0, bin, bout});
+      bin = bout;
+      k0 = k1;
+    }
+  }
+  if ((int)ch.size() > p->max_frames) return false;
+  std::stable_sort(ch.begin(), ch.end(), [](const fdlp::OlaChunk& x, const fdlp::OlaChunk& y) { return x.nf > y.nf; });
+  std::copy(ch.begin(), ch.end(), p->h_chunks);
+  *nchunks = (int)ch.size();
+  *nbounds = nb;
+  return true;
 }
 
 }  // namespace
@@ -829,6 +891,14 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
       hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&p->aux_stream, hipStreamNonBlocking) != hipSuccess)
     PLAN_FAIL(FDLP_E_NOMEM, "workspace allocation failed (reduce max_frames)");
+  if (!p->modspec && fdlp::lpc_env_can_fuse(d) &&
+      (hipMalloc((void**)&p->d_chunks, sizeof(fdlp::OlaChunk) * F) != hipSuccess ||
+       hipMalloc((void**)&p->d_bounds, sizeof(fdlp::OlaBound) * F) != hipSuccess ||
+       hipHostMalloc((void**)&p->h_chunks, sizeof(fdlp::OlaChunk) * F, hipHostMallocDefault) != hipSuccess ||
+       hipHostMalloc((void**)&p->h_bounds, sizeof(fdlp::OlaBound) * F, hipHostMallocDefault) != hipSuccess ||
+       hipMalloc((void**)&p->d_ola_counter, sizeof(int) * fdlp::kXcds) != hipSuccess ||
+       hipMalloc((void**)&p->d_ola_ring, sizeof(double) * 8 * (size_t)p->kk * (size_t)d.lpc_blocks) != hipSuccess))
+    PLAN_FAIL(FDLP_E_NOMEM, "workspace allocation failed (fused OLA tables)");
   phase(3);
 #undef PLAN_FAIL
 #undef PLAN_TRY
@@ -969,15 +1039,52 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
   }
   p->last_frames = (int)nf;
   if (nf == 0) return FDLP_OK;
-  HIP_TRY(hipMemcpyAsync(p->d_frames, p->h_frames, sizeof(fdlp::FrameDesc) * nf, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(p->d_utts, p->h_utts, sizeof(fdlp::UttDesc) * b->n_utt, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipEventRecord(p->staging_done, s));
-  p->staging_pending = true;
-
-
   // Sub-batches alternate between the caller's stream and the plan's second stream so that the
   // MFMA-bound autocorrelation of one overlaps the VALU-bound DFT / LPC kernels of the other.
   const int nsub = (int)std::max<int64_t>(1, std::min<int64_t>(p->pipeline, nf / 256));
+  // OLA + log fused into the LPC kernel on request (fdlp_set_ola_path(FUSED); the envelopes never go to HBM)
+  // unless sub-batches, the modulation spectrum or the LDS Durbin rule it out
+  int ola_nchunks = 0, ola_nbounds = 0;
+  const bool fuse = !p->modspec && p->ola_path == FDLP_OLA_FUSED && nsub == 1 && p->h_chunks &&
+                    fdlp::lpc_env_can_fuse(p->dc) && build_ola_chunks(p, b->n_utt, &ola_nchunks, &ola_nbounds);
+  if (fuse && (size_t)ola_nbounds > p->ola_fab_cap) {
+    if (p->d_ola_fab) HIP_TRY(hipFree(p->d_ola_fab));  // (the device is idle on it: staging_done waited above)
+    p->d_ola_fab = nullptr;
+    p->ola_fab_cap = 0;
+    const size_t cap = std::max<size_t>(ola_nbounds, 64);
+    HIP_TRY(hipMalloc((void**)&p->d_ola_fab, sizeof(double) * 2 * cap * p->B * p->kk));
+    p->ola_fab_cap = cap;
+  }
+  HIP_TRY(hipMemcpyAsync(p->d_frames, p->h_frames, sizeof(fdlp::FrameDesc) * nf, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(p->d_utts, p->h_utts, sizeof(fdlp::UttDesc) * b->n_utt, hipMemcpyHostToDevice, s));
+  if (fuse) {
+    HIP_TRY(hipMemcpyAsync(p->d_chunks, p->h_chunks, sizeof(fdlp::OlaChunk) * ola_nchunks, hipMemcpyHostToDevice, s));
+    if (ola_nbounds)
+      HIP_TRY(hipMemcpyAsync(p->d_bounds, p->h_bounds, sizeof(fdlp::OlaBound) * ola_nbounds, hipMemcpyHostToDevice, s));
+  }
+  HIP_TRY(hipEventRecord(p->staging_done, s));
+  p->staging_pending = true;
+  p->ola_last = p->modspec ? 0 : (fuse ? FDLP_OLA_FUSED : FDLP_OLA_SEPARATE);
+  p->env_valid = !p->modspec && (!fuse || p->debug_intermediates);
+  fdlp::OlaFused ola{};
+  if (fuse) {
+    ola.frames = p->d_frames;
+    ola.utts = p->d_utts;
+    ola.chunks = p->d_chunks;
+    ola.bounds = p->d_bounds;
+    ola.nchunks = ola_nchunks;
+    ola.nbounds = ola_nbounds;
+    ola.counter = p->d_ola_counter;
+    ola.ring = p->d_ola_ring;
+    ola.fa = p->d_ola_fab;
+    ola.fb = p->d_ola_fab ? p->d_ola_fab + p->ola_fab_cap * p->B * p->kk : nullptr;
+    ola.out = b->out_dev;
+    ola.out64 = b->out_f64_dev;
+    ola.outq = b->out_q_dev;
+    ola.qflag = b->out_q_flag_dev;
+    ola.decimals = b->ark_decimals;
+  }
+
   std::vector<hipEvent_t> ev;
   if (p->profiling) {
     if (p->prof_pending.size() >= 64) {
@@ -994,7 +1101,7 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     const size_t it0 = (size_t)f0 * B;
     const int its = n * p->B;
     double* r = p->ws.r + it0 * nl;
-    double* env = p->ws.env + it0 * p->kk;
+    double* env = fuse && !p->debug_intermediates ? nullptr : p->ws.env + it0 * p->kk;  // fused: debug copy only
     double* a_dbg = p->debug_intermediates ? p->ws.a + it0 * (p->p + 1) : nullptr;
     double* gg_dbg = p->debug_intermediates ? p->ws.gg + it0 : nullptr;
     double* cep_dbg = (p->debug_intermediates || p->modspec) ? p->ws.cep + it0 * p->M : nullptr;
@@ -1035,7 +1142,7 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     HIP_TRY(mark(3));
     HIP_TRY(fdlp::launch_lpc_env(p->dc, p->cfg.odd_mod_zero, r, its, env, a_dbg, gg_dbg, cep_dbg,
                                   p->ws.a_pad ? p->ws.a_pad + it0 * p->dc.lpc_astride : nullptr, p->ws.gg + it0,
-                                  st));
+                                  st, fuse ? &ola : nullptr));
     HIP_TRY(mark(4));
     return FDLP_OK;
   };
@@ -1060,7 +1167,7 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     HIP_TRY(fdlp::launch_modspec_out(p->ws.cep, p->d_frames, p->d_utts, (int)nf, p->B, p->M, c.coeff_0 - 1,
                                      p->feat_len, c.keep_even ? 2 : 1, keep_odd_slot, p->d_faxis,
                                      c.absolute_value, b->out_dev, b->out_f64_dev, b->ark_decimals, s));
-  } else if (!p->modspec) {  // (complex modulation: the rows were written by launch_cplx_modspec)
+  } else if (!p->modspec && !fuse) {  // (complex modulation: launch_cplx_modspec; fused: the LPC kernel)
     HIP_TRY(fdlp::launch_ola_log(p->dc, p->ws.env, p->d_frames, p->d_utts, b->n_utt, maxL, b->out_dev,
                                  b->out_f64_dev, b->out_q_dev, b->out_q_flag_dev, b->ark_decimals, s));
   }
@@ -1145,6 +1252,18 @@ int fdlp_dct_path(const fdlp_plan* p) {
   return dct_fused(p) ? FDLP_DCT_FRAME : FDLP_DCT_FOUR_STEP;
 }
 
+int fdlp_set_ola_path(fdlp_plan* p, int32_t path) {
+  if (!p || (path != FDLP_OLA_AUTO && path != FDLP_OLA_SEPARATE && path != FDLP_OLA_FUSED))
+    return fail(FDLP_E_INVALID, "fdlp_set_ola_path: FDLP_OLA_AUTO, FDLP_OLA_SEPARATE or FDLP_OLA_FUSED");
+  p->ola_path = path;
+  return FDLP_OK;
+}
+
+int fdlp_ola_path(const fdlp_plan* p) {
+  if (!p) return fail(FDLP_E_INVALID, "fdlp_ola_path: null plan");
+  return p->ola_last;
+}
+
 int fdlp_set_pipeline(fdlp_plan* p, int32_t n_sub) {
   if (!p || n_sub < 1) return fail(FDLP_E_INVALID, "fdlp_set_pipeline: need a plan and n_sub >= 1");
   p->pipeline = n_sub;
@@ -1218,6 +1337,9 @@ int fdlp_debug_fetch_range(fdlp_plan* p, int32_t f0, int32_t n, double* dct, dou
   const size_t items = (size_t)n * p->B, it0 = (size_t)f0 * p->B;
   if ((a && !p->ws.a) || (cep && !p->ws.cep))
     return fail(FDLP_E_INVALID, "fdlp_debug_fetch: a / cep are kept only after fdlp_set_debug(plan, 1)");
+  if (env && !p->env_valid)
+    return fail(FDLP_E_INVALID, "fdlp_debug_fetch: with the fused OLA the envelopes are kept only after "
+                                "fdlp_set_debug(plan, 1)");
   if (dct) HIP_TRY(hipMemcpy(dct, p->ws.dct + (size_t)f0 * p->N, sizeof(double) * n * (size_t)p->N, hipMemcpyDeviceToHost));
   if (r) HIP_TRY(hipMemcpy(r, p->ws.r + it0 * p->nlags, sizeof(double) * items * p->nlags, hipMemcpyDeviceToHost));
   if (a) HIP_TRY(hipMemcpy(a, p->ws.a + it0 * (p->p + 1), sizeof(double) * items * (p->p + 1), hipMemcpyDeviceToHost));

@@ -215,6 +215,21 @@ class FdlpPlan:
         check(lib.fdlp_plan_flat_events(self._h, None, None, ctypes.byref(n), ptr(ev, ctypes.c_int32), n.value))
         return C.value, H.value, ev
 
+    OLA_PATHS = {"auto": 0, "separate": 1, "fused": 2}
+
+    def set_ola_path(self, path: str = "auto"):
+        """'auto' / 'separate': ola_log_tiled_kernel after the LPC kernel; 'fused': OLA + log inside the LPC
+        kernel where it applies (bit-identical; measured slower; fdlp_set_ola_path)."""
+        check(lib.fdlp_set_ola_path(self._h, self.OLA_PATHS[path]))
+
+    @property
+    def ola_path(self) -> Optional[str]:
+        """The OLA stage the last compute ran: 'fused', 'separate' or None (none yet / modulation spectrum)."""
+        v = lib.fdlp_ola_path(self._h)
+        if v < 0:
+            check(v)
+        return {0: None, 1: "separate", 2: "fused"}[v]
+
     def set_pipeline(self, n_sub: int):
         check(lib.fdlp_set_pipeline(self._h, int(n_sub)))
 

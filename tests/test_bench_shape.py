@@ -37,11 +37,13 @@ def _run_batch(entries, cfg_name="wsj", pcm=None, lens=None, mix=None, max_frame
     geo = [probe.geometry(t) for t in lens]
     frames = sum(g[0] for g in geo)
     plan = FdlpPlan(cfg, device=0, max_frames=max_frames or frames)
+    plan.set_debug(True)  # (the envelopes are then kept whichever OLA stage runs)
     assert plan.autocorr_path == "structured"
     nj = sum(g[0] - 1 for g in geo)
     jit = PyRandom(7).randbits2(nj)
     _, rows, out64 = plan.compute(torch.from_numpy(pcm).cuda(), lens, jit, want_f64=True, **(mix or {}))
     torch.cuda.synchronize()
+    assert plan.ola_path == "separate"
     offs = np.concatenate([[0], np.cumsum(lens)])
     jo = np.concatenate([[0], np.cumsum([g[0] - 1 for g in geo])])
     fo = np.concatenate([[0], np.cumsum([g[0] for g in geo])])
