@@ -29,6 +29,11 @@ def main():
     ap.add_argument("--batch-frames", type=int, default=8192)
     ap.add_argument("--profile", default=None, help="write cProfile stats of the last run to this file")
     ap.add_argument("--runners", nargs="+", default=["native", "python"], choices=["native", "native_mapped", "python"])
+    ap.add_argument("--variants", nargs="+", default=["-"],
+                    help="extra CLI flags (without the leading --) per run of the native runner, e.g. "
+                         "'d2h_codes=off' 'keep_warm chunk_rows=32768'; '-' for none")
+    ap.add_argument("--repeat", type=int, default=1, help="runs per (runner, workers, variant)")
+    ap.add_argument("--trace-dir", default=None, help="native: write each run's --job_trace here")
     a = ap.parse_args()
     from bench import speech_like_batch
     from speech_recognition_tools_amd.featgen import computeFDLPSpectrogram as cli
@@ -51,10 +56,23 @@ def main():
         getFeats(build_parser().parse_args([os.path.join(d, "wav.scp"), os.path.join(d, "warm")] + opts),
                  return_feats=False)
         sys.stdout = so
-        for runner, w in [(r, w) for r in a.runners for w in a.workers]:
-            args = build_parser().parse_args([os.path.join(d, "wav.scp"), os.path.join(d, "o%d" % w),
+        runs = [(r, w, v, k) for r in a.runners for w in a.workers
+                for v in (a.variants if r.startswith("native") else [""]) for k in range(a.repeat)]
+        for runner, w, variant, rep in runs:
+            extra = ["--" + f for f in variant.split() if f != "-"]
+            if a.trace_dir and runner.startswith("native"):
+                os.makedirs(a.trace_dir, exist_ok=True)
+                tag = "%s_w%d_%s_%d" % (runner, w, "".join(ch if ch.isalnum() else "_" for ch in variant), rep)
+                extra = extra + ["--job_trace=" + os.path.join(a.trace_dir, tag + ".jsonl")]
+            # a fresh output name per run, the previous run's outputs deleted before the clock starts (replacing
+            # a 1 GB ark frees its page-cache pages inside the JOB's final rename: ~0.18 s on the box)
+            for f in os.listdir(d):
+                if f.startswith("o_"):
+                    os.remove(os.path.join(d, f))
+            oname = os.path.join(d, "o_%d_%d" % (w, rep))
+            args = build_parser().parse_args([os.path.join(d, "wav.scp"), oname,
                                               "--io_workers=%d" % w, "--host_runner=" + runner.split("_")[0]] +
-                                             (["--mapped_output"] if runner == "native_mapped" else []) + opts)
+                                             (["--mapped_output"] if runner == "native_mapped" else []) + opts + extra)
             sys.stdout = devnull
             prof = None
             if a.profile:
@@ -74,9 +92,10 @@ def main():
             audio_h = a.utts * T / 16000.0 / 3600.0
             print(json.dumps({"metric": "compute-fdlp-feats end-to-end audio-hours/s (WAV in, ark out)",
                               "value": audio_h / el, "unit": "audio-hours/s", "io_workers": w,
-                              "host_runner": runner,
+                              "host_runner": runner, "variant": variant, "repeat": rep,
+                              "batch_frames": a.batch_frames,
                               "utts": a.utts, "utt_seconds": a.seconds, "seconds": el,
-                              "ark_bytes": os.path.getsize(os.path.join(d, "o%d.ark" % w)),
+                              "ark_bytes": os.path.getsize(oname + ".ark"),
                               "job_stats": cli.LAST_JOB_STATS if runner.startswith("native") else None}))
             sys.stdout.flush()
 

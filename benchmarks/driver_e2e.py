@@ -88,7 +88,8 @@ def main():
                           "jobs_per_gpu": a.jobs_per_gpu, "ngpu": ngpu, "feats_scp_lines": n_feats,
                           "frames": frames, "job_execution_s": job_s,
                           "job_execution_s_mean": float(np.mean(job_s)) if job_s else None,
-                          "job_stats_mean": {k: float(np.mean([s[k] for s in stats])) for k in stats[0]} if stats else None,
+                          "job_stats_mean": {k: float(np.mean([s[k] for s in stats if s.get(k) is not None]))
+                                             for k in stats[0] if any(s.get(k) is not None for s in stats)} if stats else None,
                           "note": "wall from the driver's start to feats.scp; every JOB is a cold process "
                                   "(interpreter, imports, HIP init, plan build, reads, kernels, writes)"}))
 

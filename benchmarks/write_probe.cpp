@@ -1,0 +1,85 @@
+// write_probe.cpp -- how fast one ark file can be filled on the box's filesystem (the ark writer of the
+// native JOB runner, fdlp_job.cpp): one thread writing 4 MiB pieces, T threads pwrite-ing disjoint
+// ranges of the same file, and T threads copying into a shared mapping of it (ftruncate + mmap).
+//   g++ -O2 -pthread benchmarks/write_probe.cpp -o /tmp/write_probe && /tmp/write_probe <dir> [MiB]
+#include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <string>
+#include <thread>
+#include <vector>
+
+static double now_s() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+int main(int argc, char** argv) {
+  const std::string dir = argc > 1 ? argv[1] : "/tmp";
+  const size_t mib = argc > 2 ? (size_t)atol(argv[2]) : 1100;
+  const size_t n = mib << 20;
+  std::vector<char> buf(n);
+  for (size_t i = 0; i < n; i += 64) buf[i] = (char)i;
+  const std::string path = dir + "/write_probe.bin";
+  auto report = [&](const char* what, int th, double t) {
+    printf("{\"mode\": \"%s\", \"threads\": %d, \"MiB\": %zu, \"seconds\": %.4f, \"GBps\": %.2f}\n", what, th, mib, t,
+           n / t / 1e9);
+    fflush(stdout);
+  };
+  for (int rep = 0; rep < 2; ++rep) {
+    {  // one thread, write() in 4 MiB pieces
+      unlink(path.c_str());
+      const double t0 = now_s();
+      int fd = open(path.c_str(), O_CREAT | O_WRONLY | O_TRUNC, 0644);
+      for (size_t o = 0; o < n; o += 4 << 20) {
+        const size_t k = std::min<size_t>(4 << 20, n - o);
+        if (write(fd, buf.data() + o, k) != (ssize_t)k) return 1;
+      }
+      close(fd);
+      report("write", 1, now_s() - t0);
+    }
+    for (int th : {2, 4, 8}) {  // T threads, pwrite of disjoint contiguous ranges
+      unlink(path.c_str());
+      const double t0 = now_s();
+      int fd = open(path.c_str(), O_CREAT | O_WRONLY | O_TRUNC, 0644);
+      std::vector<std::thread> ts;
+      for (int t = 0; t < th; ++t)
+        ts.emplace_back([&, t] {
+          const size_t a = n * t / th, b = n * (t + 1) / th;
+          for (size_t o = a; o < b; o += 4 << 20) {
+            const size_t k = std::min<size_t>(4 << 20, b - o);
+            if (pwrite(fd, buf.data() + o, k, (off_t)o) != (ssize_t)k) abort();
+          }
+        });
+      for (auto& x : ts) x.join();
+      close(fd);
+      report("pwrite", th, now_s() - t0);
+    }
+    for (int th : {1, 4, 8}) {  // ftruncate + shared mapping, T threads memcpy
+      unlink(path.c_str());
+      const double t0 = now_s();
+      int fd = open(path.c_str(), O_CREAT | O_RDWR | O_TRUNC, 0644);
+      if (ftruncate(fd, (off_t)n) != 0) return 1;
+      char* m = (char*)mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+      if (m == MAP_FAILED) return 1;
+      std::vector<std::thread> ts;
+      for (int t = 0; t < th; ++t)
+        ts.emplace_back([&, t] {
+          const size_t a = n * t / th, b = n * (t + 1) / th;
+          memcpy(m + a, buf.data() + a, b - a);
+        });
+      for (auto& x : ts) x.join();
+      munmap(m, n);
+      close(fd);
+      report("mmap", th, now_s() - t0);
+    }
+  }
+  unlink(path.c_str());
+  return 0;
+}

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define FDLP_ABI_VERSION 7
+#define FDLP_ABI_VERSION 8
 
 enum {
   FDLP_OK = 0,
@@ -400,6 +400,18 @@ typedef struct fdlp_job_opts {
   const char* cmvn_path;       /* non-NULL: global CMVN stats (Kaldi binary DM) of the written features */
   int32_t out_mapped;          /* 1: the OLA kernel stores the features straight into the pinned host
                                   slots (no D2H copy); 0 (default): device buffer + D2H copy (ABI 4)   */
+  /* ---- ABI 8 ---- */
+  int32_t out_codes;           /* D2H leg as int16 ark codes (fdlp_batch.out_q_dev), widened to the
+                                  float32 ark values on the host by a thread pool: -1 auto (codes when
+                                  0 <= ark_decimals <= 3 and not out_mapped), 0 float32, 1 codes.  A
+                                  batch whose codes overflow is copied again as float32 (same arks)  */
+  int32_t chunk_rows;          /* feature rows per D2H piece (0: 65536); the writer starts on a batch's
+                                  first piece while the rest are still in flight                     */
+  int32_t keep_warm;           /* 1: keep the plan, streams and pinned slots of this call for the next
+                                  call in the process with the same config (fdlp_job_release frees
+                                  them); 0: release them on return                                    */
+  const char* trace_path;      /* non-NULL: JSON lines of the JOB's pipeline events (seconds since the
+                                  call started; benchmarks/job_timeline.py summarises them)           */
 } fdlp_job_opts;
 typedef struct fdlp_job_stats {
   int64_t n_lines;             /* scp entries                                  */
@@ -415,9 +427,19 @@ typedef struct fdlp_job_stats {
   double plan_seconds;         /* fdlp_plan_create (part of setup)              */
   double pinned_seconds;       /* pinned host buffers of the first slot (setup); the
                                   other slots are pinned by a helper thread      */
+  /* ---- ABI 8 ---- */
+  double d2h_wait_seconds;     /* widening stage waiting for D2H pieces to land  */
+  double widen_seconds;        /* widening stage busy (codes -> float32)        */
+  int64_t n_batches;           /* device batches                               */
+  int64_t n_code_fallbacks;    /* batches copied again as float32 (code overflow) */
+  int32_t codes;               /* 1: the D2H leg carried int16 codes            */
+  int32_t warm;                /* 1: plan and slots came from the previous call */
 } fdlp_job_stats;
 int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_path, const char* outfile,
                  const fdlp_job_opts* opts, fdlp_job_stats* stats);
+/* Frees what a keep_warm call parked (plan, streams, pinned and device slots); a no-op when nothing
+ * is parked.  Call before destroying the HIP context of the process. */
+int fdlp_job_release(void);
 
 #ifdef __cplusplus
 }

@@ -39,7 +39,7 @@ FDLP_MODE_MODSPEC_COMPLEX = 2
 FDLP_WIN_HAMMING = 0
 FDLP_WIN_HANNING = 1
 FDLP_WIN_RECT = 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 STAGE_NAMES = ("frames_dft1", "dft2_dct", "autocorr", "lpc_env", "ola_log")
 
 c_i32, c_i64, c_dbl, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
@@ -96,6 +96,7 @@ class FdlpJobOptsC(ctypes.Structure):
         ("io_threads", c_i32), ("preprocess", c_i32), ("noise", P_i16), ("noise_len", c_i64), ("snr", c_dbl),
         ("noise_seed", ctypes.c_uint32), ("jitter_key", P_u32), ("jitter_key_len", c_i32), ("srate", c_i32),
         ("progress_name", ctypes.c_char_p), ("cmvn_path", ctypes.c_char_p), ("out_mapped", c_i32),
+        ("out_codes", c_i32), ("chunk_rows", c_i32), ("keep_warm", c_i32), ("trace_path", ctypes.c_char_p),
     ]
 
 
@@ -104,7 +105,8 @@ class FdlpJobStatsC(ctypes.Structure):
         ("n_lines", c_i64), ("n_done", c_i64), ("n_skipped", c_i64), ("n_frames_out", c_i64),
         ("n_samples", c_i64), ("seconds", c_dbl), ("setup_seconds", c_dbl), ("read_wait_seconds", c_dbl),
         ("write_seconds", c_dbl), ("slot_wait_seconds", c_dbl), ("plan_seconds", c_dbl),
-        ("pinned_seconds", c_dbl),
+        ("pinned_seconds", c_dbl), ("d2h_wait_seconds", c_dbl), ("widen_seconds", c_dbl),
+        ("n_batches", c_i64), ("n_code_fallbacks", c_i64), ("codes", c_i32), ("warm", c_i32),
     ]
 
 
@@ -155,6 +157,7 @@ SIGNATURES = {
     "fdlp_wav_decode": (c_i32, [P_u8, c_i64, P_i32, P_i32, P_i32, P_i64, P_dbl]),
     "fdlp_job_run": (c_i32, [ctypes.POINTER(FdlpConfigC), c_i32, ctypes.c_char_p, ctypes.c_char_p,
                              ctypes.POINTER(FdlpJobOptsC), ctypes.POINTER(FdlpJobStatsC)]),
+    "fdlp_job_release": (c_i32, []),
     "fdlp_ark_open": (c_i32, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(c_p)]),
     "fdlp_ark_write": (c_i32, [c_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), c_i32, c_i32]),
     "fdlp_ark_close": (c_i32, [c_p]),

@@ -22,4 +22,6 @@ struct ArkItem {
   int32_t rows;
 };
 int ark_write_batch(fdlp_ark_writer* w, const ArkItem* items, size_t n, int32_t cols);
+// n int16 ark codes -> the float32 ark values (fdlp_q_widen on the calling thread, table lookups)
+void q_widen_span(const int16_t* q, int64_t n, int32_t decimals, float* out);
 }  // namespace fdlp

@@ -408,6 +408,15 @@ int fdlp_ark_write(fdlp_ark_writer* w, const char* utt, const float* mat, int32_
 }  // extern "C" (the batch writer below is internal C++)
 
 namespace fdlp {
+void q_widen_span(const int16_t* q, int64_t n, int32_t decimals, float* out) {
+  double scale10 = 1.0;
+  for (int i = 0; i < decimals; ++i) scale10 *= 10.0;
+  q_widen_range(q, n, q_table(decimals, scale10), scale10, out);
+}
+}  // namespace fdlp
+
+
+namespace fdlp {
 int ark_write_batch(fdlp_ark_writer* w, const ArkItem* items, size_t n, int32_t cols) {
   if (!w || (n && !items) || cols < 0) return fail(FDLP_E_INVALID, "ark_write_batch: bad args");
   if (fflush(w->ark) != 0) return w->failed = true, fail(FDLP_E_IO, "ark write failed");

@@ -22,6 +22,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -335,39 +336,129 @@ class Reader {
   std::vector<std::thread> th_;
 };
 
-// ---- writer thread ----------------------------------------------------------------------------
-struct Done {
-  int slot;
-  std::vector<std::string> ids;
-  std::vector<int64_t> rows;  // n + 1 row offsets into the slot's host output
+// ---- pipeline trace (fdlp_job_opts.trace_path) --------------------------------------------------
+struct Trace {
+  bool on = false;
+  double t0 = 0.0;
+  struct Ev {
+    double t;
+    const char* what;
+    int64_t a, b;
+  };
+  std::mutex m;
+  std::vector<Ev> ev;
+  void add(const char* what, int64_t a = 0, int64_t b = 0) {
+    if (!on) return;
+    const double t = now_s() - t0;
+    std::lock_guard<std::mutex> g(m);
+    ev.push_back({t, what, a, b});
+  }
+  void dump(const char* path) {
+    if (!on || !path) return;
+    FILE* f = fopen(path, "w");
+    if (!f) return;
+    for (const Ev& e : ev)
+      fprintf(f, "{\"t\": %.6f, \"ev\": \"%s\", \"a\": %lld, \"b\": %lld}\n", e.t, e.what, (long long)e.a,
+              (long long)e.b);
+    fclose(f);
+  }
 };
 
+// ---- part pool: f(0..parts-1) on a few threads and the caller (one caller at a time) --------------
+class PartPool {
+ public:
+  explicit PartPool(int n) {
+    for (int t = 0; t < n; ++t) th_.emplace_back([this] { loop(); });
+  }
+  ~PartPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int threads() const { return (int)th_.size() + 1; }
+  void run(int parts, const std::function<void(int)>& f) {
+    if (th_.empty() || parts <= 1) {
+      for (int i = 0; i < parts; ++i) f(i);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      f_ = &f;
+      parts_ = parts;
+      next_ = 0;
+      left_ = parts;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [&] { return left_ == 0; });
+    f_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const std::function<void(int)>* fn;
+      int i;
+      {
+        std::lock_guard<std::mutex> g(m_);
+        if (!f_ || next_ >= parts_) return;
+        fn = f_;
+        i = next_++;
+      }
+      (*fn)(i);
+      std::lock_guard<std::mutex> g(m_);
+      if (--left_ == 0) done_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* f_ = nullptr;
+  int parts_ = 0, next_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+  std::vector<std::thread> th_;
+};
+
+// ---- batch slots --------------------------------------------------------------------------------
+constexpr int kSlots = 3;
+constexpr int kMaxPieces = 16;   // D2H pieces per batch (one event each)
+constexpr int kRing = 4;         // widened pieces in flight between the widening stage and the writer
+
 struct Slot {
-  int kind = FDLP_PCM_I16;
   void* h_pcm = nullptr;       // pinned
   size_t pcm_cap = 0;          // bytes
   void* d_pcm = nullptr;
   size_t d_pcm_cap = 0;
-  float* h_out = nullptr;      // pinned
-  float* d_out = nullptr;
-  size_t out_cap = 0;          // floats
-  hipEvent_t done = nullptr;     // the batch's features are in h_out
+  float* d_out = nullptr;      // the batch's float32 features (the code fallback and the CMVN source)
+  size_t out_cap = 0;          // bytes
+  int16_t* d_q = nullptr;      // int16 ark codes (codes mode)
+  size_t q_cap = 0;            // bytes
+  uint32_t* d_qflag = nullptr;
+  void* h_dl = nullptr;        // pinned landing buffer of the D2H leg: codes, or float32 features
+  size_t dl_cap = 0;           // bytes
+  uint32_t* h_qflag = nullptr; // pinned
   hipEvent_t ev_in = nullptr;    // its PCM is on the device
   hipEvent_t ev_comp = nullptr;  // its features are computed
+  hipEvent_t ev_piece[kMaxPieces] = {};  // piece j of the D2H leg has landed
   bool busy = false;           // in flight or not yet written
-  bool pinned = false;         // h_pcm / h_out allocated (by the pinning thread)
-};
-
-struct JobState {
-  std::mutex m;
-  std::condition_variable cv;
-  std::deque<Done> queue;
-  bool finish = false;
-  int err = FDLP_OK;
-  std::string err_msg;
-  std::vector<Slot>* slots = nullptr;
-  int pin_err = FDLP_OK;       // pinning thread failure
-  std::string pin_msg;
+  bool pinned = false;         // h_pcm / h_dl allocated (by the pinning thread)
 };
 
 int grow_pinned(void** p, size_t* cap, size_t need) {
@@ -393,7 +484,142 @@ int grow_device(void** p, size_t* cap, size_t need, hipStream_t s) {
   return FDLP_OK;
 }
 
+void free_slot(Slot& sl) {
+  if (sl.h_pcm) (void)hipHostFree(sl.h_pcm);
+  if (sl.h_dl) (void)hipHostFree(sl.h_dl);
+  if (sl.h_qflag) (void)hipHostFree(sl.h_qflag);
+  if (sl.d_pcm) (void)hipFree(sl.d_pcm);
+  if (sl.d_out) (void)hipFree(sl.d_out);
+  if (sl.d_q) (void)hipFree(sl.d_q);
+  if (sl.d_qflag) (void)hipFree(sl.d_qflag);
+  if (sl.ev_in) (void)hipEventDestroy(sl.ev_in);
+  if (sl.ev_comp) (void)hipEventDestroy(sl.ev_comp);
+  for (auto& e : sl.ev_piece)
+    if (e) (void)hipEventDestroy(e);
+  sl = Slot();
+}
+
+// ---- what a keep_warm call leaves for the next one -------------------------------------------------
+// The plan, the streams and the slots (pinned and device buffers, events) of a JOB, keyed by the
+// config bytes (lifter values compared separately), the device and the batch size.
+struct Warm {
+  fdlp_config key{};
+  std::vector<double> lifter;
+  int device = -1;
+  fdlp_plan* plan = nullptr;
+  hipStream_t s = nullptr, s_in = nullptr, s_out = nullptr;
+  std::vector<Slot> slots;
+};
+std::mutex g_warm_m;
+Warm* g_warm = nullptr;
+
+fdlp_config warm_key(const fdlp_config& c) {
+  fdlp_config k;
+  memcpy(&k, &c, sizeof k);
+  k.lifter = nullptr;
+  return k;
+}
+
+void free_warm(Warm* w) {
+  if (!w) return;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(w->device);
+  for (hipStream_t x : {w->s, w->s_in, w->s_out})
+    if (x) (void)hipStreamSynchronize(x);
+  for (auto& sl : w->slots) free_slot(sl);
+  for (hipStream_t x : {w->s, w->s_in, w->s_out})
+    if (x) (void)hipStreamDestroy(x);
+  fdlp_plan_destroy(w->plan);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  delete w;
+}
+
+// the parked state if it matches (key, lifter values, device); a parked state that does not is freed
+Warm* take_warm(const fdlp_config& c, int device) {
+  Warm* w;
+  {
+    std::lock_guard<std::mutex> g(g_warm_m);
+    w = g_warm;
+    g_warm = nullptr;
+  }
+  if (!w) return nullptr;
+  const fdlp_config k = warm_key(c);
+  bool same = w->device == device && memcmp(&k, &w->key, sizeof k) == 0 && (c.lifter != nullptr) == !w->lifter.empty();
+  if (same && c.lifter) same = memcmp(c.lifter, w->lifter.data(), sizeof(double) * (size_t)c.coeff_num) == 0;
+  if (same) return w;
+  free_warm(w);
+  return nullptr;
+}
+
+// utterance boundaries of the D2H pieces of a batch: whole utterances, about chunk_rows rows each, at
+// most kMaxPieces pieces
+std::vector<int32_t> piece_bounds(const std::vector<int64_t>& rows /* n + 1 offsets */, int64_t chunk_rows) {
+  const int32_t n = (int32_t)rows.size() - 1;
+  const int64_t total = rows.back();
+  const int64_t target = std::max<int64_t>(chunk_rows, (total + kMaxPieces - 1) / kMaxPieces);
+  std::vector<int32_t> cb{0};
+  int64_t start = 0;
+  for (int32_t i = 1; i < n; ++i)
+    if (rows[i] - start >= target && (int)cb.size() < kMaxPieces) {
+      cb.push_back(i);
+      start = rows[i];
+    }
+  cb.push_back(n);
+  return cb;
+}
+
+// one finished batch on its way to the ark
+struct Done {
+  int slot = 0;
+  int64_t batch = 0;
+  std::vector<std::string> ids;
+  std::vector<int64_t> rows;   // n + 1 row offsets into the batch's features
+  std::vector<int32_t> cb;     // piece boundaries (utterance indices), pieces = cb.size() - 1
+  bool codes = false;
+  bool mapped = false;
+  bool fallback = false;       // codes overflowed: the float32 features were copied instead, into fb
+  std::vector<float> fb;
+};
+
+struct Piece {
+  std::shared_ptr<Done> d;
+  int j = 0;
+  const float* data = nullptr;  // rows of piece j (nullptr: skip, an error is pending)
+  int ring = -1;
+};
+
+struct JobState {
+  std::mutex m;
+  std::condition_variable cv;        // consumer <-> stages, slot releases, pinning
+  std::deque<std::shared_ptr<Done>> queue;   // consumer -> widening stage
+  std::deque<Piece> pieces;          // widening stage -> writer
+  bool finish_a = false, finish_b = false;
+  bool ring_busy[kRing] = {false, false, false, false};
+  int err = FDLP_OK;
+  std::string err_msg;
+  int pin_err = FDLP_OK;             // pinning thread failure
+  std::string pin_msg;
+  void set_err(int e, const std::string& msg) {  // caller holds m
+    if (err == FDLP_OK) {
+      err = e;
+      err_msg = msg;
+    }
+  }
+};
+
 }  // namespace
+
+extern "C" int fdlp_job_release(void) {
+  Warm* w;
+  {
+    std::lock_guard<std::mutex> g(g_warm_m);
+    w = g_warm;
+    g_warm = nullptr;
+  }
+  free_warm(w);
+  return FDLP_OK;
+}
 
 extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_path, const char* outfile,
                             const fdlp_job_opts* o, fdlp_job_stats* st) {
@@ -401,9 +627,20 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   if (o->scp_type != 0 && o->scp_type != 1) return fail(FDLP_E_INVALID, "Invalid type of scp type, it should be either wav or segment");
   if (cfg->mode != FDLP_MODE_SPECTROGRAM) return fail(FDLP_E_INVALID, "fdlp_job_run: spectrogram plans only");
   if (o->noise && o->preprocess == FDLP_PRE_DIFF) return fail(FDLP_E_INVALID, "fdlp_job_run: diff and noise are exclusive");
+  if (o->out_codes < -1 || o->out_codes > 1) return fail(FDLP_E_INVALID, "fdlp_job_run: out_codes must be -1, 0 or 1");
+  if (o->out_codes == 1 && (o->ark_decimals < 0 || o->out_mapped))
+    return fail(FDLP_E_INVALID, "fdlp_job_run: out_codes needs ark_decimals >= 0 and no out_mapped");
   const double t_start = now_s();
   fdlp_job_stats stats{};
-  double write_busy = 0.0;
+  double write_busy = 0.0, widen_busy = 0.0, d2h_wait = 0.0;
+  Trace trace;
+  trace.on = o->trace_path != nullptr;
+  trace.t0 = t_start;
+  const bool mapped = o->out_mapped != 0;
+  const bool codes = o->out_codes == 1 || (o->out_codes == -1 && !mapped && o->ark_decimals >= 0 && o->ark_decimals <= 3);
+  const size_t dl_elem = codes ? sizeof(int16_t) : sizeof(float);
+  const int64_t chunk_rows = o->chunk_rows > 0 ? o->chunk_rows : 65536;
+  stats.codes = codes ? 1 : 0;
 
   // scp lines (for line in fid: every line, blank lines included, is an entry of the reference; a
   // blank line raises IndexError there; here blank lines are ignored like the Python drop-in)
@@ -435,36 +672,40 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   const int hop0 = (int)((double)c.srate / (1.0 / (ov * c.fduration)));
   const size_t pin_smp = (size_t)c.max_frames * (size_t)(std::max(hop0, 1) + 1);
   const size_t pin_rows = (size_t)c.max_frames * (size_t)((int64_t)hop0 * c.frate / std::max(1, c.srate) + 2);
-  const size_t pin_out_bytes = pin_rows * (size_t)std::max(1, c.nfilters) * sizeof(float);
-  std::vector<Slot> slots(3);
-  std::vector<size_t> hout_cap(slots.size(), 0);  // bytes of each slot's pinned output
+  const size_t pin_dl_bytes = pin_rows * (size_t)std::max(1, c.nfilters) * dl_elem;
+
+  Warm* warm = take_warm(c, device);
+  stats.warm = warm ? 1 : 0;
+  std::vector<Slot> slots = warm ? std::move(warm->slots) : std::vector<Slot>(kSlots);
+  for (auto& sl : slots) sl.pinned = false;  // usable once the pinning thread has checked (or grown) its buffers
   JobState js;
-  js.slots = &slots;
-  // pinning thread: page-locking the three slots' host buffers (~0.4 GB) overlaps the plan creation and
-  // the first reads; slot k becomes usable when slots[k].pinned is set
+  // pinning thread: page-locking the slots' host buffers overlaps the plan creation and the first reads;
+  // slot k becomes usable when slots[k].pinned is set (slots of a warm call are pinned already)
   std::thread pinner([&] {
     for (size_t k = 0; k < slots.size(); ++k) {
       const double t0 = now_s();
-      void* hp = nullptr;
-      size_t cap = 0;
-      float* ho = nullptr;
-      int e = grow_pinned(&hp, &cap, pin_smp * sizeof(int16_t));
-      if (e == FDLP_OK && hipHostMalloc((void**)&ho, pin_out_bytes, hipHostMallocDefault) != hipSuccess)
+      void* hp = slots[k].h_pcm;
+      size_t pcap = slots[k].pcm_cap;
+      void* hd = slots[k].h_dl;
+      size_t dcap = slots[k].dl_cap;
+      uint32_t* hf = slots[k].h_qflag;
+      int e = grow_pinned(&hp, &pcap, pin_smp * sizeof(int16_t));
+      if (e == FDLP_OK) e = grow_pinned(&hd, &dcap, pin_dl_bytes);
+      if (e == FDLP_OK && !hf && hipHostMalloc((void**)&hf, 64, hipHostMallocDefault) != hipSuccess)
         e = fail(FDLP_E_NOMEM, "pinned host allocation failed");
       std::lock_guard<std::mutex> g(js.m);
       if (k == 0) stats.pinned_seconds = now_s() - t0;
+      slots[k].h_pcm = hp;
+      slots[k].pcm_cap = pcap;
+      slots[k].h_dl = hd;
+      slots[k].dl_cap = dcap;
+      slots[k].h_qflag = hf;
       if (e != FDLP_OK) {
-        if (hp) (void)hipHostFree(hp);
-        if (ho) (void)hipHostFree(ho);
         js.pin_err = e;
         js.pin_msg = fdlp::last_error_slot();
         js.cv.notify_all();
         return;
       }
-      slots[k].h_pcm = hp;
-      slots[k].pcm_cap = cap;
-      slots[k].h_out = ho;
-      hout_cap[k] = pin_out_bytes;
       slots[k].pinned = true;
       js.cv.notify_all();
     }
@@ -472,16 +713,21 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   auto join_pinner = [&] {
     if (pinner.joinable()) pinner.join();
   };
-  fdlp_plan* plan = nullptr;
+  fdlp_plan* plan = warm ? warm->plan : nullptr;
+  hipStream_t s = warm ? warm->s : nullptr, s_in = warm ? warm->s_in : nullptr,
+              s_out = warm ? warm->s_out : nullptr;  // compute, copy-in, copy-out
+  const fdlp_config key = warm_key(c);
+  std::vector<double> key_lifter;
+  if (c.lifter) key_lifter.assign(c.lifter, c.lifter + c.coeff_num);
+  delete warm;
+  warm = nullptr;
   const double t_plan = now_s();
-  int rc = fdlp_plan_create(&c, device, &plan);
+  int rc = plan ? FDLP_OK : fdlp_plan_create(&c, device, &plan);
   stats.plan_seconds = now_s() - t_plan;
+  trace.add("plan");
   if (rc != FDLP_OK) {
     join_pinner();
-    for (auto& sl : slots) {
-      if (sl.h_pcm) (void)hipHostFree(sl.h_pcm);
-      if (sl.h_out) (void)hipHostFree(sl.h_out);
-    }
+    for (auto& sl : slots) free_slot(sl);
     return rc;
   }
   int32_t B = 0;
@@ -489,46 +735,42 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
 
   int prev_dev = -1;
   (void)hipGetDevice(&prev_dev);
-  hipStream_t s = nullptr, s_in = nullptr, s_out = nullptr;  // compute, copy-in, copy-out
   fdlp_pyrandom* jrng = nullptr;
   fdlp_nprandom* nrng = nullptr;
   fdlp_ark_writer* ark = nullptr;
   int16_t* d_noise = nullptr;
   double* d_cmvn = nullptr;
+  hipStream_t s_fb = nullptr;  // the float32 copy of a batch whose codes overflowed
   CopyPool copies(4);  // before cleanup(): drained there before the pinned buffers are freed
+  PartPool widen_pool(codes ? 5 : 0);
+  std::vector<std::vector<float>> ring(kRing);
   std::string len_text;
-  std::thread writer;
+  std::thread stage_a, stage_b;
   int32_t sr_seen = -1;  // 'sr' of the last successful read (:139; NameError before the first one)
 
   auto cleanup = [&](int code) -> int {
     std::string keep = code != FDLP_OK ? fdlp::last_error_slot() : std::string();
+    trace.add("cleanup");
     join_pinner();
-    if (writer.joinable()) {
-      {
-        std::lock_guard<std::mutex> g(js.m);
-        js.finish = true;
-      }
-      js.cv.notify_all();
-      writer.join();
+    {
+      std::lock_guard<std::mutex> g(js.m);
+      js.finish_a = true;
     }
-    if (s) (void)hipStreamSynchronize(s);
-    if (s_in) (void)hipStreamSynchronize(s_in);
-    if (s_out) (void)hipStreamSynchronize(s_out);
+    js.cv.notify_all();
+    if (stage_a.joinable()) stage_a.join();
+    {
+      std::lock_guard<std::mutex> g(js.m);
+      js.finish_b = true;
+    }
+    js.cv.notify_all();
+    if (stage_b.joinable()) stage_b.join();
+    for (hipStream_t x : {s, s_in, s_out, s_fb})
+      if (x) (void)hipStreamSynchronize(x);
     for (int k = 0; k < (int)slots.size(); ++k) copies.wait(k);
-    for (auto& sl : slots) {
-      if (sl.h_pcm) (void)hipHostFree(sl.h_pcm);
-      if (sl.h_out) (void)hipHostFree(sl.h_out);
-      if (sl.d_pcm) (void)hipFree(sl.d_pcm);
-      if (sl.d_out) (void)hipFree(sl.d_out);
-      if (sl.done) (void)hipEventDestroy(sl.done);
-      if (sl.ev_in) (void)hipEventDestroy(sl.ev_in);
-      if (sl.ev_comp) (void)hipEventDestroy(sl.ev_comp);
-    }
+    trace.add("joined");
     if (d_noise) (void)hipFree(d_noise);
     if (d_cmvn) (void)hipFree(d_cmvn);
-    if (s) (void)hipStreamDestroy(s);
-    if (s_in) (void)hipStreamDestroy(s_in);
-    if (s_out) (void)hipStreamDestroy(s_out);
+    if (s_fb) (void)hipStreamDestroy(s_fb);
     if (jrng) fdlp_pyrandom_destroy(jrng);
     if (nrng) fdlp_nprandom_destroy(nrng);
     if (ark && code != FDLP_OK) {
@@ -540,11 +782,45 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
         keep = fdlp::last_error_slot();
       }
     }
-    fdlp_plan_destroy(plan);
+    trace.add("closed");
+    bool parked = false;
+    if (o->keep_warm && code == FDLP_OK && s && s_in && s_out) {  // park for the next call
+      bool all_pinned = true;
+      for (auto& sl : slots) all_pinned = all_pinned && sl.pinned && !sl.busy;
+      if (all_pinned) {
+        Warm* w = new Warm();
+        w->key = key;
+        w->lifter = key_lifter;
+        w->device = device;
+        w->plan = plan;
+        w->s = s;
+        w->s_in = s_in;
+        w->s_out = s_out;
+        w->slots = std::move(slots);
+        Warm* old;
+        {
+          std::lock_guard<std::mutex> g(g_warm_m);
+          old = g_warm;
+          g_warm = w;
+        }
+        free_warm(old);
+        parked = true;
+      }
+    }
+    if (!parked) {
+      for (auto& sl : slots) free_slot(sl);
+      for (hipStream_t x : {s, s_in, s_out})
+        if (x) (void)hipStreamDestroy(x);
+      fdlp_plan_destroy(plan);
+    }
     if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
     stats.seconds = now_s() - t_start;
     stats.write_seconds = write_busy;
+    stats.widen_seconds = widen_busy;
+    stats.d2h_wait_seconds = d2h_wait;
     if (st) *st = stats;
+    trace.add("end");
+    trace.dump(o->trace_path);
     if (code != FDLP_OK) fdlp::last_error_slot() = keep;
     return code;
   };
@@ -552,13 +828,15 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
 #define JOB_HIP(expr) do { hipError_t e_ = (expr); if (e_ != hipSuccess) return cleanup(fail(FDLP_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_))); } while (0)
 
   JOB_HIP(hipSetDevice(device));
-  JOB_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  JOB_HIP(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking));
-  JOB_HIP(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking));
+  if (!s) JOB_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  if (!s_in) JOB_HIP(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking));
+  if (!s_out) JOB_HIP(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking));
   for (auto& sl : slots) {
-    JOB_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
-    JOB_HIP(hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming));
-    JOB_HIP(hipEventCreateWithFlags(&sl.ev_comp, hipEventDisableTiming));
+    if (!sl.ev_in) JOB_HIP(hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming));
+    if (!sl.ev_comp) JOB_HIP(hipEventCreateWithFlags(&sl.ev_comp, hipEventDisableTiming));
+    for (auto& e : sl.ev_piece)
+      if (!e) JOB_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (codes && !sl.d_qflag) JOB_HIP(hipMalloc((void**)&sl.d_qflag, 64));
   }
   JOB_TRY(fdlp_pyrandom_create(o->jitter_key, o->jitter_key_len, &jrng));
   if (o->noise) {
@@ -570,48 +848,131 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     JOB_HIP(hipMalloc((void**)&d_cmvn, sizeof(double) * 2 * (B + 1)));
     JOB_HIP(hipMemsetAsync(d_cmvn, 0, sizeof(double) * 2 * (B + 1), s));
   }
+  if (codes) JOB_HIP(hipStreamCreateWithFlags(&s_fb, hipStreamNonBlocking));
   const std::string out_s(outfile);
   JOB_TRY(fdlp_ark_open((out_s + ".ark").c_str(), (out_s + ".scp").c_str(), &ark));
 
-  // writer: ark/scp + .len of finished batches, in order
-  writer = std::thread([&] {
+  // stage A (landing + widening): waits for each D2H piece, widens codes into a ring buffer on the part
+  // pool (or passes the float32 rows through), and hands the piece to the writer in order
+  stage_a = std::thread([&] {
+    int64_t seq = 0;
     for (;;) {
-      Done d;
+      std::shared_ptr<Done> d;
       {
         std::unique_lock<std::mutex> g(js.m);
-        js.cv.wait(g, [&] { return js.finish || !js.queue.empty(); });
+        js.cv.wait(g, [&] { return js.finish_a || !js.queue.empty(); });
         if (js.queue.empty()) return;
-        d = std::move(js.queue.front());
+        d = js.queue.front();
         js.queue.pop_front();
       }
-      Slot& sl = slots[d.slot];
+      Slot& sl = slots[d->slot];
+      const int np = (int)d->cb.size() - 1;
+      bool bad = false;
+      for (int j = 0; j < np; ++j) {
+        const double tw = now_s();
+        if (!bad && hipEventSynchronize(sl.ev_piece[j]) != hipSuccess) {
+          std::lock_guard<std::mutex> g(js.m);
+          js.set_err(FDLP_E_HIP, "device batch failed");
+          bad = true;
+        }
+        d2h_wait += now_s() - tw;
+        trace.add("landed", d->batch, j);
+        const int64_t r0 = d->rows[d->cb[j]], r1 = d->rows[d->cb[j + 1]];
+        const size_t nv = (size_t)(r1 - r0) * (size_t)B;
+        Piece pc;
+        pc.d = d;
+        pc.j = j;
+        if (!bad && j == 0 && d->codes && *sl.h_qflag) {  // a code overflowed: the batch's float32 features
+          const size_t tot = (size_t)d->rows.back() * (size_t)B;
+          d->fb.resize(tot);
+          if (hipMemcpyAsync(d->fb.data(), sl.d_out, sizeof(float) * tot, hipMemcpyDeviceToHost, s_fb) != hipSuccess ||
+              hipStreamSynchronize(s_fb) != hipSuccess) {
+            std::lock_guard<std::mutex> g(js.m);
+            js.set_err(FDLP_E_HIP, "D2H copy failed");
+            bad = true;
+          }
+          d->fallback = true;
+          std::lock_guard<std::mutex> g(js.m);
+          ++stats.n_code_fallbacks;
+        }
+        if (bad) {
+          pc.data = nullptr;
+        } else if (!d->codes) {
+          pc.data = (const float*)sl.h_dl + (size_t)r0 * B;
+        } else if (d->fallback) {
+          pc.data = d->fb.data() + (size_t)r0 * B;
+        } else {
+          const int k = (int)(seq++ % kRing);
+          {
+            std::unique_lock<std::mutex> g(js.m);
+            js.cv.wait(g, [&] { return !js.ring_busy[k]; });
+            js.ring_busy[k] = true;
+          }
+          if (ring[k].size() < nv) ring[k].resize(nv);
+          const double t0 = now_s();
+          const int16_t* q = (const int16_t*)sl.h_dl + (size_t)r0 * B;
+          float* out = ring[k].data();
+          const int parts = (int)std::max<size_t>(1, std::min<size_t>((size_t)widen_pool.threads(), nv >> 17));
+          widen_pool.run(parts, [&](int i) {
+            const size_t a = nv * (size_t)i / parts, b = nv * (size_t)(i + 1) / parts;
+            fdlp::q_widen_span(q + a, (int64_t)(b - a), o->ark_decimals, out + a);
+          });
+          widen_busy += now_s() - t0;
+          trace.add("widened", d->batch, j);
+          pc.data = out;
+          pc.ring = k;
+        }
+        {
+          std::lock_guard<std::mutex> g(js.m);
+          js.pieces.push_back(std::move(pc));
+        }
+        js.cv.notify_all();
+      }
+    }
+  });
+
+  // stage B (writer): ark/scp + .len of the pieces, in order; frees the slot after its last piece
+  stage_b = std::thread([&] {
+    std::vector<fdlp::ArkItem> items;
+    for (;;) {
+      Piece pc;
+      {
+        std::unique_lock<std::mutex> g(js.m);
+        js.cv.wait(g, [&] { return js.finish_b || !js.pieces.empty(); });
+        if (js.pieces.empty()) return;
+        pc = std::move(js.pieces.front());
+        js.pieces.pop_front();
+      }
+      Done& d = *pc.d;
+      const double tb = now_s();
       int err = FDLP_OK;
       std::string msg;
-      if (hipEventSynchronize(sl.done) != hipSuccess) {
-        err = FDLP_E_HIP;
-        msg = "device batch failed";
-      }
-      const double tb = now_s();
-      if (err == FDLP_OK) {
-        std::vector<fdlp::ArkItem> items(d.ids.size());
-        for (size_t i = 0; i < d.ids.size(); ++i) {
+      if (pc.data) {
+        const int32_t u0 = d.cb[pc.j], u1 = d.cb[pc.j + 1];
+        const int64_t base = d.rows[u0];
+        items.resize((size_t)(u1 - u0));
+        for (int32_t i = u0; i < u1; ++i) {
           const int64_t r0 = d.rows[i], r1 = d.rows[i + 1];
-          items[i] = {d.ids[i].c_str(), sl.h_out + r0 * B, (int32_t)(r1 - r0)};
+          items[i - u0] = {d.ids[i].c_str(), pc.data + (r0 - base) * B, (int32_t)(r1 - r0)};
           if (o->write_len) len_text += d.ids[i] + " " + std::to_string(r1 - r0) + "\n";  // :235-236
         }
-        if (fdlp::ark_write_batch(ark, items.data(), items.size(), B) != FDLP_OK) {
+        bool skip;
+        {
+          std::lock_guard<std::mutex> g(js.m);
+          skip = js.err != FDLP_OK;
+        }
+        if (!skip && fdlp::ark_write_batch(ark, items.data(), items.size(), B) != FDLP_OK) {
           err = FDLP_E_IO;
           msg = fdlp::last_error_slot();
         }
       }
       write_busy += now_s() - tb;
+      trace.add("written", d.batch, pc.j);
       {
         std::lock_guard<std::mutex> g(js.m);
-        sl.busy = false;
-        if (err != FDLP_OK && js.err == FDLP_OK) {
-          js.err = err;
-          js.err_msg = msg;
-        }
+        if (pc.ring >= 0) js.ring_busy[pc.ring] = false;
+        if (pc.j + 2 == (int)d.cb.size()) slots[d.slot].busy = false;
+        if (err != FDLP_OK) js.set_err(err, msg);
       }
       js.cv.notify_all();
     }
@@ -627,6 +988,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     int kind = FDLP_PCM_I16;
   } pend;
   int slot_i = 0;
+  int64_t n_batch = 0;
   int32_t ramp = std::max(64, c.max_frames / 8);  // frames of the current batch (see the loop)
 
   // waits until the slot's previous batch is written, then makes it the current one
@@ -644,18 +1006,21 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   auto flush = [&]() -> int {
     if (pend.ids.empty()) return FDLP_OK;
     Slot& sl = slots[slot_i];
+    trace.add("flush", n_batch, pend.frames);
     const size_t elem = pend.kind == FDLP_PCM_I16 ? pcm_elem_i16 : pcm_elem_f64;
     copies.wait(slot_i);  // every utterance of the batch is in the pinned buffer
+    trace.add("copies", n_batch);
+    const size_t nval = (size_t)pend.out_rows * B;
     int r = grow_device(&sl.d_pcm, &sl.d_pcm_cap, (size_t)pend.samples * elem, s);
     if (r != FDLP_OK) return r;
     // out_mapped: the OLA kernel stores the features straight into the slot's pinned host buffer (mapped
     // into the device address space), no D2H copy; with --cmvn_stats they stay in device memory for the
-    // statistics kernel.  Default: device buffer + D2H copy on the copy-out stream
+    // statistics kernel.  Otherwise: device features (+ codes) and a D2H leg in pieces on the copy-out stream
     float* h_out_dev = nullptr;
-    if (o->out_mapped && !d_cmvn && hipHostGetDevicePointer((void**)&h_out_dev, sl.h_out, 0) != hipSuccess)
-      h_out_dev = nullptr;
+    if (mapped && !d_cmvn && hipHostGetDevicePointer((void**)&h_out_dev, sl.h_dl, 0) != hipSuccess) h_out_dev = nullptr;
     if (!h_out_dev) {
-      r = grow_device((void**)&sl.d_out, &sl.out_cap, sizeof(float) * (size_t)pend.out_rows * B, s);
+      r = grow_device((void**)&sl.d_out, &sl.out_cap, sizeof(float) * nval, s);
+      if (r == FDLP_OK && codes) r = grow_device((void**)&sl.d_q, &sl.q_cap, sizeof(int16_t) * nval, s);
       if (r != FDLP_OK) return r;
     }
     // copy-in on its own stream so it overlaps the previous batch's kernels
@@ -677,25 +1042,44 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     b.out_f64_dev = nullptr;
     b.ark_decimals = o->ark_decimals;
     b.preprocess = o->preprocess;
+    const bool use_codes = codes && !h_out_dev;
+    b.out_q_dev = use_codes ? sl.d_q : nullptr;
+    b.out_q_flag_dev = use_codes ? sl.d_qflag : nullptr;
+    if (use_codes && hipMemsetAsync(sl.d_qflag, 0, sizeof(uint32_t), s) != hipSuccess)  // the caller zeroes it
+      return fail(FDLP_E_HIP, "flag reset failed");
     r = fdlp_compute(plan, &b, s);
     if (r != FDLP_OK) return r;
     if (d_cmvn) {
       r = fdlp_cmvn_accumulate(sl.d_out, pend.out_rows, B, d_cmvn, s);
       if (r != FDLP_OK) return r;
     }
-    if (h_out_dev) {  // the features are in h_out once the compute stream passes this point
-      if (hipEventRecord(sl.done, s) != hipSuccess) return fail(FDLP_E_HIP, "event record failed");
-    } else if (hipEventRecord(sl.ev_comp, s) != hipSuccess || hipStreamWaitEvent(s_out, sl.ev_comp, 0) != hipSuccess ||
-               hipMemcpyAsync(sl.h_out, sl.d_out, sizeof(float) * (size_t)pend.out_rows * B, hipMemcpyDeviceToHost,
-                              s_out) != hipSuccess ||
-               hipEventRecord(sl.done, s_out) != hipSuccess) {  // copy-out on its own stream (overlaps the next batch)
-      return fail(FDLP_E_HIP, "D2H copy failed");
+    auto d = std::make_shared<Done>();
+    d->slot = slot_i;
+    d->batch = n_batch;
+    d->codes = use_codes;
+    d->mapped = h_out_dev != nullptr;
+    d->rows = std::move(pend.rows);
+    d->rows.push_back(pend.out_rows);
+    if (h_out_dev) {  // the features are in h_dl once the compute stream passes this point
+      d->cb = {0, (int32_t)pend.ids.size()};
+      if (hipEventRecord(sl.ev_piece[0], s) != hipSuccess) return fail(FDLP_E_HIP, "event record failed");
+    } else {
+      d->cb = piece_bounds(d->rows, chunk_rows);
+      if (hipEventRecord(sl.ev_comp, s) != hipSuccess || hipStreamWaitEvent(s_out, sl.ev_comp, 0) != hipSuccess)
+        return fail(FDLP_E_HIP, "event record failed");
+      if (use_codes && hipMemcpyAsync(sl.h_qflag, sl.d_qflag, sizeof(uint32_t), hipMemcpyDeviceToHost, s_out) != hipSuccess)
+        return fail(FDLP_E_HIP, "D2H copy failed");
+      const char* src = use_codes ? (const char*)sl.d_q : (const char*)sl.d_out;
+      for (size_t j = 0; j + 1 < d->cb.size(); ++j) {  // copy-out on its own stream (overlaps the next batch)
+        const size_t r0 = (size_t)d->rows[d->cb[j]], r1 = (size_t)d->rows[d->cb[j + 1]];
+        const size_t off = r0 * B * dl_elem, n = (r1 - r0) * B * dl_elem;
+        if ((n && hipMemcpyAsync((char*)sl.h_dl + off, src + off, n, hipMemcpyDeviceToHost, s_out) != hipSuccess) ||
+            hipEventRecord(sl.ev_piece[j], s_out) != hipSuccess)
+          return fail(FDLP_E_HIP, "D2H copy failed");
+      }
     }
-    Done d;
-    d.slot = slot_i;
-    d.ids = std::move(pend.ids);
-    d.rows = std::move(pend.rows);
-    d.rows.push_back(pend.out_rows);
+    trace.add("launched", n_batch, (int64_t)d->cb.size() - 1);
+    d->ids = std::move(pend.ids);
     {
       std::lock_guard<std::mutex> g(js.m);
       sl.busy = true;
@@ -704,6 +1088,8 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     js.cv.notify_all();
     if (o->progress_name) fflush(stdout);
     pend = Pending();
+    ++n_batch;
+    ++stats.n_batches;
     slot_i = (slot_i + 1) % (int)slots.size();
     return acquire_slot(slot_i);
   };
@@ -714,11 +1100,13 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     for (size_t k = 0; k < slots.size(); ++k) {
       Slot& sl = slots[k];
       JOB_TRY(grow_device(&sl.d_pcm, &sl.d_pcm_cap, smp * sizeof(int16_t), s));
-      if (!o->out_mapped || o->cmvn_path) JOB_TRY(grow_device((void**)&sl.d_out, &sl.out_cap, rows * B * sizeof(float), s));
+      if (!mapped || o->cmvn_path) JOB_TRY(grow_device((void**)&sl.d_out, &sl.out_cap, rows * B * sizeof(float), s));
+      if (codes) JOB_TRY(grow_device((void**)&sl.d_q, &sl.q_cap, rows * B * sizeof(int16_t), s));
     }
   }
 
   stats.setup_seconds = now_s() - t_start;
+  trace.add("setup");
   for (size_t i = 0; i < reader.size(); ++i) {
     const double tw = now_s();
     Utt& u = reader.get(i);
@@ -762,7 +1150,12 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
       JOB_HIP(hipStreamSynchronize(s));
       {
         std::unique_lock<std::mutex> g(js.m);
-        js.cv.wait(g, [&] { return js.queue.empty() || js.err != FDLP_OK; });
+        js.cv.wait(g, [&] {
+          if (js.err != FDLP_OK) return true;
+          for (auto& sl : slots)
+            if (sl.busy) return false;
+          return true;
+        });
       }
       fdlp_plan_destroy(plan);
       plan = nullptr;
@@ -785,14 +1178,16 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
       copies.submit(slot_i, (int16_t*)sl.h_pcm + pend.samples, u.s16, sizeof(int16_t) * T, u.raw);
     else
       copies.submit(slot_i, (double*)sl.h_pcm + pend.samples, u.f64->data(), sizeof(double) * T, u.f64);
-    // pinned host output for this batch's rows
+    // pinned landing buffer for this batch's rows (float32 in mapped mode: the OLA kernel stores into it)
     const size_t rows_need = (size_t)(pend.out_rows + L);
-    if (rows_need * B * sizeof(float) > hout_cap[slot_i]) {
-      const size_t nb = std::max(rows_need * B * sizeof(float), (size_t)c.max_frames * 120 * B * sizeof(float));
-      if (sl.h_out) (void)hipHostFree(sl.h_out);
-      sl.h_out = nullptr;
-      JOB_HIP(hipHostMalloc((void**)&sl.h_out, nb, hipHostMallocDefault));
-      hout_cap[slot_i] = nb;
+    const size_t land_elem = mapped ? sizeof(float) : dl_elem;
+    if (rows_need * B * land_elem > sl.dl_cap) {
+      const size_t nb = std::max(rows_need * B * land_elem, (size_t)c.max_frames * 120 * B * land_elem);
+      if (sl.h_dl) (void)hipHostFree(sl.h_dl);
+      sl.h_dl = nullptr;
+      sl.dl_cap = 0;
+      JOB_HIP(hipHostMalloc((void**)&sl.h_dl, nb, hipHostMallocDefault));
+      sl.dl_cap = nb;
     }
     pend.kind = kind;
     pend.ids.push_back(u.id);
@@ -813,21 +1208,19 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     reader.done(i);
   }
   JOB_TRY(flush());
-  {
-    std::unique_lock<std::mutex> g(js.m);
-    js.cv.wait(g, [&] { return js.queue.empty() || js.err != FDLP_OK; });
-    if (js.err != FDLP_OK) return cleanup(fail(js.err, js.err_msg));
-  }
-  JOB_HIP(hipStreamSynchronize(s));
+  trace.add("read_all");
   {  // wait for the writer to finish the last batches
     std::unique_lock<std::mutex> g(js.m);
     js.cv.wait(g, [&] {
+      if (js.err != FDLP_OK) return true;
       for (auto& sl : slots)
-        if (sl.busy) return js.err != FDLP_OK;
+        if (sl.busy) return false;
       return true;
     });
     if (js.err != FDLP_OK) return cleanup(fail(js.err, js.err_msg));
   }
+  trace.add("drained");
+  JOB_HIP(hipStreamSynchronize(s));
   if (o->write_len) {  // <outfile>.len (:232-237), written whole then renamed
     const std::string tmp = out_s + ".len.tmp";
     FILE* f = fopen(tmp.c_str(), "w");

@@ -1,0 +1,68 @@
+"""Start the HIP runtime of a cold compute-fdlp-feats JOB on a helper thread.
+
+A cold JOB process (make_FDLPspectrum_feats.sh:126-172 starts `nj` of them) spends ~0.2-0.25 s in the
+HIP runtime's first calls (device enumeration, queues, the first copy; benchmarks/hip_init_probe.hip)
+and ~0.1 s importing numpy and the package.  computeFDLPSpectrogram.py calls start(argv) before its
+heavy imports: the argv is parsed with the real parser (featgen/_fdlp_args.py, no numpy), the JOB's GPU
+is made the only visible one exactly as main() would do it, and a daemon thread loads the HIP runtime
+(the libamdhip64.so.7 libfdlp_hip.so binds to) and makes one small allocation and copy, so the runtime
+start overlaps the imports.  The ctypes calls release the GIL.  main() joins the thread before exit.
+Nothing happens unless the native JOB runner will run (no torch in the process, no --add_reverb).
+"""
+import ctypes
+import os
+import sys
+import threading
+import time
+
+NARROWED = False   # HIP_VISIBLE_DEVICES was narrowed here (main() then addresses the GPU as device 0)
+T_START = None     # time.perf_counter() when the helper started / finished (the JOB's job_stats report them)
+T_DONE = None
+_thread = None
+
+
+def _warm():
+    global T_DONE
+    try:
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        n = ctypes.c_int(0)
+        if hip.hipGetDeviceCount(ctypes.byref(n)) != 0 or n.value < 1:
+            return
+        if hip.hipSetDevice(0) != 0:
+            return
+        p = ctypes.c_void_p()
+        if hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(256)) != 0:
+            return
+        buf = ctypes.create_string_buffer(256)
+        hip.hipMemcpy(p, buf, ctypes.c_size_t(256), 1)  # hipMemcpyHostToDevice
+        hip.hipFree(p)
+    except (OSError, AttributeError):
+        pass  # no runtime here: the JOB reports it from its own first HIP call
+    T_DONE = time.perf_counter()
+
+
+def start(argv):
+    global NARROWED, _thread, T_START
+    if _thread is not None or "torch" in sys.modules:
+        return
+    from speech_recognition_tools_amd.featgen._fdlp_args import build_parser, narrow_visible_devices, native_eligible
+    try:
+        args, _ = build_parser().parse_known_args(argv)
+    except SystemExit:
+        return  # main() prints the usage error
+    try:
+        if not native_eligible(args):
+            return
+        if "CUDA_VISIBLE_DEVICES" not in os.environ:
+            narrow_visible_devices(args)
+            NARROWED = True
+    except ValueError:
+        return  # main() raises it
+    T_START = time.perf_counter()
+    _thread = threading.Thread(target=_warm, name="hip-runtime-start", daemon=True)
+    _thread.start()
+
+
+def join():
+    if _thread is not None:
+        _thread.join()

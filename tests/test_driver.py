@@ -255,3 +255,29 @@ def test_resume_guard(tmp_path):
     r = subprocess.run(["bash", guard, str(key), str(stamp), str(out), str(extra), "--", "touch", str(mark)],
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and not mark.exists()
+
+
+def test_early_hip_start_narrows_like_main(monkeypatch):
+    """A cold JOB parses its argv with the real parser before numpy is imported (featgen/_early_hip.py):
+    the native runner's GPU becomes the only visible one exactly as main() would narrow it, main() then
+    addresses it as device 0, and the python runner / --add_reverb leave the environment alone."""
+    import sys
+    from speech_recognition_tools_amd.featgen import _early_hip
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "LOCAL_RANK"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setattr(_early_hip, "NARROWED", False)
+    monkeypatch.setattr(_early_hip, "_thread", None)
+    monkeypatch.setattr(_early_hip, "_warm", lambda: None)  # no HIP runtime start in the CPU suite
+    had_torch = sys.modules.pop("torch", None)
+    try:
+        for argv in (["a.scp", "o", "--host_runner=python"], ["a.scp", "o", "--add_reverb=small_room"]):
+            _early_hip.start(argv)
+            assert not _early_hip.NARROWED and "HIP_VISIBLE_DEVICES" not in os.environ
+        monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1,2,3")
+        _early_hip.start(["a.scp", "o", "--device_rr=3,4"])
+        assert _early_hip.NARROWED and os.environ["HIP_VISIBLE_DEVICES"] == "2"
+        _early_hip.join()
+    finally:
+        if had_torch is not None:
+            sys.modules["torch"] = had_torch
+        monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)

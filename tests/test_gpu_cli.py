@@ -239,6 +239,54 @@ def test_native_runner_batch_ramp_matches_python(tmp_path):
     assert len(open(a + ".len").read().split("\n")) == 301
 
 
+def test_native_runner_d2h_legs_write_identical_arks(tmp_path):
+    """The native runner's device-to-host leg in every form writes the Python loop's bytes: float32 rows,
+    int16 ark codes widened on the host (in one piece and in many small pieces), codes that overflow
+    (--ark_precision 4 leaves most log values outside int16: every batch is copied again as float32),
+    the mapped-output path, and a second call that reuses the first one's plan and pinned slots."""
+    from speech_recognition_tools_amd.featgen import computeFDLPSpectrogram as cli
+    meta, _, _, _ = load_golden("wsj")
+    rng = np.random.default_rng(5)
+    utts = ["d%04d" % i for i in range(90)]
+    sig = {u: np.clip(rng.standard_normal(int(rng.integers(16000, 80000))) * 3000, -32768, 32767).astype(np.int16)
+           for u in utts}
+    scp = _write_scp(str(tmp_path), sig, utts)
+    base = [scp] + _opts(meta) + ["--batch_frames=256"]
+
+    def run(name, extra, runner="native"):
+        out = str(tmp_path / name)
+        _run([base[0], out] + base[1:] + extra, runner)
+        return (open(out + ".ark", "rb").read(), open(out + ".len").read(),
+                [(l.split()[0], l.split()[1].rsplit(":", 1)[1]) for l in open(out + ".scp")])
+
+    for prec in (3, 4):
+        want = run("py%d" % prec, ["--ark_precision=%d" % prec], "python")
+        cases = {"off": ["--d2h_codes=off"], "on": ["--d2h_codes=on"],
+                 "on_pieces": ["--d2h_codes=on", "--chunk_rows=300"], "mapped": ["--mapped_output"]}
+        for name, extra in cases.items():
+            got = run("n%d_%s" % (prec, name), ["--ark_precision=%d" % prec] + extra)
+            assert got == want, (prec, name)
+            st = cli.LAST_JOB_STATS
+            assert st["codes"] == (1 if name.startswith("on") else 0), (prec, name)
+            if name == "on_pieces":
+                assert st["n_batches"] >= 3
+            if name.startswith("on"):
+                fb = st["n_code_fallbacks"]
+                assert (fb >= 1) if prec == 4 else fb == 0, (prec, name, fb, st["n_batches"])
+    # keep_warm: the second call takes the parked plan and slots and writes the same bytes
+    trace = str(tmp_path / "trace.jsonl")
+    a = run("w1", ["--keep_warm"])
+    assert cli.LAST_JOB_STATS["warm"] == 0
+    b = run("w2", ["--keep_warm", "--job_trace=" + trace])
+    assert cli.LAST_JOB_STATS["warm"] == 1 and a == b
+    from speech_recognition_tools_amd import _lib
+    _lib.lib.fdlp_job_release()
+    import json
+    ev = [json.loads(l)["ev"] for l in open(trace)]
+    for e in ("plan", "setup", "flush", "launched", "landed", "widened", "written", "end"):
+        assert e in ev, e
+
+
 @RUNNERS
 def test_cli_diff_and_noise(tmp_path, monkeypatch, runner):
     meta, sig, ref, z = load_golden("wsj_diff")
