@@ -32,6 +32,10 @@ WSJ_OPTS = ["--nfilters", "80", "--order", "150", "--fduration", "1.5", "--frate
             "--coeff_range", "0,100", "--overlap_fraction", "0.25", "--fbank_type", "cochlear,1,1,1,2.5,1",
             "--write_utt2num_frames", "true",  # e2e/wsj/run_fdlp_e1.sh:54-95
             "--add_opts", "--job_stats"]       # per-JOB phase timings into the JOB logs
+# the same features as the CLI's own options (a JOB the driver would start)
+WSJ_OPTS_CLI = ["--nfilters=80", "--order=150", "--fduration=1.5", "--frate=100", "--coeff_num=100",
+                "--coeff_range=0,100", "--overlap_fraction=0.25", "--fbank_type=cochlear,1,1,1,2.5,1",
+                "--write_utt2num_frames"]
 
 
 def main():
@@ -80,13 +84,36 @@ def main():
                 if ": job stats " in line:
                     stats.append(json.loads(line.split(": job stats ", 1)[1]))
         audio_h = sum(lens) / 16000.0 / 3600.0
+        # one cold JOB process timed from outside (interpreter start to exit) on a shard of the same size
+        shard = os.path.join(base, "one_job.scp")
+        lines = open(os.path.join(data, "wav.scp")).read().splitlines(True)
+        with open(shard, "w") as f:
+            f.writelines(lines[:max(1, len(lines) // a.nj)])
+        cli = os.path.join(ROOT, "speech_recognition_tools_amd", "featgen", "computeFDLPSpectrogram.py")
+        one = {}
+        for k in range(2):
+            t1 = time.perf_counter()
+            r1 = subprocess.run(["python3", cli, shard, os.path.join(base, "one_job_%d" % k)] + WSJ_OPTS_CLI + ["--job_stats"],
+                                cwd=base, capture_output=True, text=True)
+            w1 = time.perf_counter() - t1
+            if r1.returncode != 0:
+                sys.stderr.write(r1.stdout[-2000:] + r1.stderr[-2000:])
+                sys.exit(r1.returncode)
+            ex = [float(l.split()[2]) for l in r1.stdout.splitlines() if l.startswith("Execution Time:")]
+            js = [json.loads(l.split(": job stats ", 1)[1]) for l in r1.stdout.splitlines() if ": job stats " in l]
+            one.setdefault("process_wall_s", []).append(round(w1, 4))
+            one.setdefault("execution_time_s", []).append(ex[0] if ex else None)
+            if js:
+                one.setdefault("early_hip_start_s", []).append(js[0].get("early_hip_start_s"))
+                one.setdefault("early_hip_done_s", []).append(js[0].get("early_hip_done_s"))
+                one.setdefault("plan_s", []).append(js[0].get("plan_seconds"))
         from speech_recognition_tools_amd.shard import visible_gpu_count
         ngpu = a.ngpu or max(1, visible_gpu_count())  # the driver's own rule
         print(json.dumps({"metric": "recipe stage-1 end-to-end audio-hours/s (make_FDLPspectrum_feats.sh, cold JOBs)",
                           "value": audio_h / wall, "unit": "audio-hours/s", "wall_s": wall, "audio_hours": audio_h,
                           "utts": a.utts, "utt_seconds": "U(%g,%g)" % tuple(a.lengths), "nj": a.nj,
                           "jobs_per_gpu": a.jobs_per_gpu, "ngpu": ngpu, "feats_scp_lines": n_feats,
-                          "frames": frames, "job_execution_s": job_s,
+                          "frames": frames, "job_execution_s": job_s, "one_cold_job": one,
                           "job_execution_s_mean": float(np.mean(job_s)) if job_s else None,
                           "job_stats_mean": {k: float(np.mean([s[k] for s in stats if s.get(k) is not None]))
                                              for k in stats[0] if any(s.get(k) is not None for s in stats)} if stats else None,

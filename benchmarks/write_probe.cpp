@@ -44,6 +44,29 @@ int main(int argc, char** argv) {
       close(fd);
       report("write", 1, now_s() - t0);
     }
+    for (size_t piece : {(size_t)1 << 20, (size_t)64 << 20}) {  // one thread, other piece sizes
+      unlink(path.c_str());
+      const double t0 = now_s();
+      int fd = open(path.c_str(), O_CREAT | O_WRONLY | O_TRUNC, 0644);
+      for (size_t o = 0; o < n; o += piece) {
+        const size_t k = std::min(piece, n - o);
+        if (write(fd, buf.data() + o, k) != (ssize_t)k) return 1;
+      }
+      close(fd);
+      report(piece == ((size_t)1 << 20) ? "write_1MiB" : "write_64MiB", 1, now_s() - t0);
+    }
+    {  // fallocate the whole size first, then one thread writes 4 MiB pieces
+      unlink(path.c_str());
+      const double t0 = now_s();
+      int fd = open(path.c_str(), O_CREAT | O_WRONLY | O_TRUNC, 0644);
+      const int fa = posix_fallocate(fd, 0, (off_t)n);
+      for (size_t o = 0; o < n; o += 4 << 20) {
+        const size_t k = std::min<size_t>(4 << 20, n - o);
+        if (pwrite(fd, buf.data() + o, k, (off_t)o) != (ssize_t)k) return 1;
+      }
+      close(fd);
+      report(fa == 0 ? "fallocate_write" : "fallocate_failed_write", 1, now_s() - t0);
+    }
     for (int th : {2, 4, 8}) {  // T threads, pwrite of disjoint contiguous ranges
       unlink(path.c_str());
       const double t0 = now_s();

@@ -7,7 +7,7 @@
 # HIP -- HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES if set, else the KFD
 # topology's GPU nodes -- so a recipe that calls the driver unchanged, e.g. --cmd "$train_cmd" --nj 20
 # (e2e/wsj/run_fdlp_e1.sh:196), spreads its JOBs over the node), --jobs_per_gpu K (without $cmd: at most
-# N*K JOBs run at once; default 2), --job_mem / --job_gpu (the resource request a $cmd launcher gets for
+# N*K JOBs run at once; default 4), --job_mem / --job_gpu (the resource request a $cmd launcher gets for
 # every JOB: "$cmd --mem 5G --gpu 1 JOB=1:$nj ...", the reference's --mem 5G (:92, :141) plus one GPU, so
 # queue.pl / slurm.pl allocate the MI355X the JOB runs on; run.pl ignores both; --job_gpu 0 drops it),
 # --resume true (per-JOB resume: every JOB that finishes leaves <feat_dir>/melspec_<name>.JOB.done holding
@@ -42,7 +42,9 @@ write_utt2num_frames=false
 lifter_config=
 check_for_segment="data/train"
 ngpu=          # default: the visible GPU count (visible_gpus below)
-jobs_per_gpu=2  # two JOBs per GPU overlap each other's latency-bound kernels
+jobs_per_gpu=4  # JOBs per GPU at once: their kernels overlap on the device and the cold
+               # processes' fixed costs (interpreter, HIP runtime start) overlap each other: 8 cold JOBs on
+               # one GPU 0.71 / 1.03 / 1.09 audio-h/s at 2 / 4 / 8 (profiles/r05k_driver_jobs_per_gpu.jsonl)
 compute_cmvn=false   # also write <data_dir>/cmvn.ark (global CMVN stats, fused on the device)
 seed=
 noise_seed=
