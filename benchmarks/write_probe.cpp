@@ -3,6 +3,7 @@
 // ranges of the same file, and T threads copying into a shared mapping of it (ftruncate + mmap).
 //   g++ -O2 -pthread benchmarks/write_probe.cpp -o /tmp/write_probe && /tmp/write_probe <dir> [MiB]
 #include <fcntl.h>
+#include <linux/falloc.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -66,6 +67,20 @@ int main(int argc, char** argv) {
       }
       close(fd);
       report(fa == 0 ? "fallocate_write" : "fallocate_failed_write", 1, now_s() - t0);
+    }
+    for (int keep : {1, 0}) {  // fallocate each 21 MiB piece just before writing it (KEEP_SIZE or extending)
+      const size_t piece = (size_t)21 << 20;
+      unlink(path.c_str());
+      const double t0 = now_s();
+      int fd = open(path.c_str(), O_CREAT | O_WRONLY | O_TRUNC, 0644);
+      bool ok = true;
+      for (size_t o = 0; o < n; o += piece) {
+        const size_t k = std::min(piece, n - o);
+        ok = ok && fallocate(fd, keep ? FALLOC_FL_KEEP_SIZE : 0, (off_t)o, (off_t)k) == 0;
+        if (write(fd, buf.data() + o, k) != (ssize_t)k) return 1;
+      }
+      close(fd);
+      report(!ok ? "piece_fallocate_failed" : keep ? "piece_fallocate_keep_size" : "piece_fallocate_extend", 1, now_s() - t0);
     }
     for (int th : {2, 4, 8}) {  // T threads, pwrite of disjoint contiguous ranges
       unlink(path.c_str());

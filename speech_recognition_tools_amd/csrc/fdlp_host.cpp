@@ -12,6 +12,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <fcntl.h>
+#include <linux/falloc.h>
 #include <sys/uio.h>
 #include <unistd.h>
 
@@ -460,6 +462,10 @@ int ark_write_batch(fdlp_ark_writer* w, const ArkItem* items, size_t n, int32_t 
         return w->failed = true, fail(FDLP_E_IO, "scp write failed");
       total += hl + dl;
     }
+    // reserve the blocks of this writev first (one allocation call instead of block by block as the
+    // page cache fills; 10.2-10.7 -> 11.6-12.6 GB/s on the MI355X box's overlay, profiles/r05m_*); a
+    // filesystem without fallocate just writes
+    (void)fallocate(fd, FALLOC_FL_KEEP_SIZE, pos, (off_t)total);
     size_t k = 0;  // writev until every iovec is out (it may write partially)
     while (k < iov.size()) {
       const int cnt = (int)std::min<size_t>(iov.size() - k, IOV_MAX);
