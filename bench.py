@@ -872,6 +872,13 @@ def main():
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_unit": "bytes/launch (rocprofv3 PMC, %s)" % os.path.relpath(pmc_file or "none", ROOT),
                      "avg_launch_ms": dom_ms, "algorithmic_flops_per_launch": stage_flops[dom],
+                     "timing": ("avg_launch_ms = HIP events recorded around the stage's kernels on the stream they "
+                                "run on (fdlp_stage_times), one batch in flight, mean over the %d profiled steps of "
+                                "this run; achieved = algorithmic_flops_per_launch / avg_launch_ms.  The events "
+                                "include the launch gaps between the stage's kernels, so a kernel-trace sum of "
+                                "the kernels below is at most this (scripts/round_evidence.sh writes both side "
+                                "by side: <tag>_frac_check.json)" % args.steps),
+                     "stage_kernels": list(stage_kernel_prefixes(dom, path)),
                      "stage_fracs": {k: stage_flops[k] / (stage_ms[k] * 1e-3) / 1e12 / FP64_PEAK_TFLOPS
                                      for k in stage_ms if stage_ms[k] > 0},
                      "canonical_frac": ac_can * frames / (sms["autocorr"] * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,

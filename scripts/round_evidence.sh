@@ -14,6 +14,11 @@ mkdir -p $O
 BARGS=${BENCH_ARGS:-"--steps 5 --warmup 1 --no-cpu-baseline --inflight 1 --no-transfers"}
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3 bench.py $BARGS > $O/trace.log 2>&1 || { echo "trace failed"; tail -20 $O/trace.log; exit 3; }
 python3 scripts/rocpd_summary.py $O/trace/run_results.db $O/kernel_trace_stats.csv > /dev/null || true
+# the trace run's own bench line (its HIP-event stage times come from the same process as the kernel trace)
+# and the dominant stage's frac recomputed from the trace's kernel durations beside the HIP-event one
+tail -1 $O/trace.log > $O/trace_bench_line.json
+python3 scripts/frac_check.py $O/trace_bench_line.json $O/kernel_trace_stats.csv > $O/frac_check.json || true
+cp $O/frac_check.json profiles/${TAG}_frac_check.json 2>/dev/null || true
 i=0
 for pmc in FETCH_SIZE WRITE_SIZE "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU" "SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS" ${EXTRA_PMC:-}; do
   i=$((i+1))
