@@ -31,9 +31,19 @@ for k,m in d.items():
     print('%-50s %6.3f ms valu %5.1f%% mfma %5.1f%% lds %.3g conf %.3g GB %.2f' % (k.replace('void ','')[:50], m.get('avg_ms',0), m.get('valu_active_pct_per_simd',0), m.get('mfma_busy_pct',0), m.get('SQ_INSTS_LDS',0), m.get('SQ_LDS_BANK_CONFLICT',0), (m.get('fetch_bytes_x2',0)+m.get('write_bytes',0))/1e9))
 " gpurun_out/evidence_$TAG/pmc.json
 fi
-timeout -k 10 600 python3 bench.py > $O/bench_full.log 2>&1 || { echo "bench failed"; tail -20 $O/bench_full.log; exit 5; }
-tail -1 $O/bench_full.log > $O/bench_full.json
-for c in ${CONFIGS:-reverb chime4}; do
+if [ -z "${NO_WSJ_BENCH:-}" ]; then
+  timeout -k 10 600 python3 bench.py > $O/bench_full.log 2>&1 || { echo "bench failed"; tail -20 $O/bench_full.log; exit 5; }
+  tail -1 $O/bench_full.log > $O/bench_full.json
+fi
+if [ -n "${REVERB_PMC:-}" ]; then  # the REVERB trace + PMC passes -> profiles/${TAG}_reverb_pmc.json (the REVERB line's traffic)
+  SKIP_BENCH=1 EXTRA_PMC="SQ_WAIT_INST_LDS+SQ_WAIT_ANY+SQ_BUSY_CYCLES+SQ_WAVE_CYCLES" TAG=${TAG}_reverb \
+    BENCH_ARGS="--config reverb --steps 3 --warmup 1 --no-cpu-baseline --inflight 1 --no-transfers" bash scripts/round_evidence.sh || exit 7
+fi
+if [ -n "${LIBRI:-}" ]; then
+  timeout -k 10 400 python3 bench.py --workload librispeech --no-cpu-baseline > $O/bench_librispeech.log 2>&1 || { echo "bench librispeech failed"; tail -30 $O/bench_librispeech.log; exit 8; }
+  tail -1 $O/bench_librispeech.log > $O/bench_librispeech.json
+fi
+for c in ${CONFIGS-reverb chime4}; do
   timeout -k 10 400 python3 bench.py --config $c --no-cpu-baseline > $O/bench_$c.log 2>&1 || { echo "bench $c failed"; tail -30 $O/bench_$c.log; exit 6; }
   tail -1 $O/bench_$c.log > $O/bench_$c.json
 done
