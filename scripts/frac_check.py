@@ -16,7 +16,7 @@ import sys
 
 
 def main():
-    line = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+    line = [json.loads(x) for x in open(sys.argv[1]) if x.lstrip().startswith("{") and '"roofline"' in x][-1]
     rf = line["roofline"]
     pre = rf.get("stage_kernels") or []
     flops, peak = rf["algorithmic_flops_per_launch"], rf["peak"]

@@ -16,7 +16,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3
 python3 scripts/rocpd_summary.py $O/trace/run_results.db $O/kernel_trace_stats.csv > /dev/null || true
 # the trace run's own bench line (its HIP-event stage times come from the same process as the kernel trace)
 # and the dominant stage's frac recomputed from the trace's kernel durations beside the HIP-event one
-tail -1 $O/trace.log > $O/trace_bench_line.json
+grep '"roofline"' $O/trace.log | tail -1 > $O/trace_bench_line.json
 python3 scripts/frac_check.py $O/trace_bench_line.json $O/kernel_trace_stats.csv > $O/frac_check.json || true
 cp $O/frac_check.json profiles/${TAG}_frac_check.json 2>/dev/null || true
 i=0
