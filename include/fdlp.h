@@ -322,6 +322,12 @@ int fdlp_reverb(const fdlp_reverb_batch* batch, void* stream);
 int fdlp_cmvn_accumulate(const float* feats_dev, int64_t rows, int32_t dim, double* stats_dev,
                          void* stream);
 
+/* ---- the OLA stage's device log (for accuracy tests) ---------------------------------------- */
+/* y_dev[i] = the log the OLA stage applies to its clipped sums (computeFDLPSpectrogram.py:227 np.log),
+ * for n fp64 values x_dev[i] > 0 (NaN / +inf pass through): a table + polynomial log within ~0.5 ulp
+ * (fdlp_device.h ola_log).  ABI 8. */
+int fdlp_device_log(const double* x_dev, double* y_dev, int64_t n, void* stream);
+
 /* ---- host-side RNG replicas (no device work) --------------------------------------------- */
 /* CPython `random` (MT19937, init_by_array seeding, randrange(2) = getrandbits(2) with
  * rejection) -- the jitter source of computeFDLPSpectrogram.py:21,225. */

@@ -162,6 +162,7 @@ SIGNATURES = {
     "fdlp_ark_write": (c_i32, [c_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), c_i32, c_i32]),
     "fdlp_ark_close": (c_i32, [c_p]),
     "fdlp_ark_abort": (c_i32, [c_p]),
+    "fdlp_device_log": (c_i32, [c_p, c_p, c_i64, c_p]),
     "fdlp_cmvn_accumulate": (c_i32, [c_p, c_i64, c_i32, c_p, c_p]),
     "fdlp_reverb": (c_i32, [ctypes.POINTER(FdlpReverbBatchC), c_p]),
     "fdlp_mel_plan_create": (c_i32, [ctypes.POINTER(FdlpMelConfigC), c_i32, ctypes.POINTER(c_p)]),

@@ -8,6 +8,7 @@
 #include <stdint.h>
 
 #include "fdlp_internal.h"
+#include "fdlp_logtab.h"
 
 namespace fdlp {
 
@@ -298,10 +299,47 @@ __device__ __forceinline__ int16_t q_code(double k, bool& bad) {
 // One feature of the OLA output (computeFDLPSpectrogram.py:227-229): log(clip(acc, 1e-14)) keeping NaN,
 // stored as fp64 (debug), float32 ('%.<d>f'-rounded when decimals >= 0) and / or compact code; the OLA
 // kernel, the fused OLA of the lattice kernel and the boundary fixup all store through this.
+// np.log of the OLA sums (computeFDLPSpectrogram.py:227) in ~35 VALU operations instead of the ~65 of
+// ocml's log: x = 2^e m with m in [sqrt(1/2), sqrt(2)) (so e = 0 around 1: no ln 2 cancellation),
+// i = round(128 m), c = i / 128, u = m - c exactly (Sterbenz), r = u RN(1/c) (|r| < 2^-7.5),
+// log x = e ln2 + log c + log1p(r), log1p(r) by its degree-8 Taylor polynomial (truncation < 1e-19 r);
+// e ln2_hi (exact: 42-bit ln2_hi) + log(c)_hi summed error-free (TwoSum, kept out of FMA contraction by the
+// _rn intrinsics), then the small terms once: within ~0.5 ulp (tests/test_device_log.py: <= 1 ulp against
+// numpy's log over 1e-14 .. 1e12).  NaN and +inf pass through.  lt = kLogTable (fdlp_logtab.h) or a copy
+// of it in LDS.
+__device__ __forceinline__ double ola_log(double x, const double* __restrict__ lt) {
+  constexpr double kSqrtHalf = 0.70710678118654752440;
+  int e = __builtin_amdgcn_frexp_exp(x);
+  double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
+  if (m < kSqrtHalf) {
+    m = 2.0 * m;
+    --e;
+  }
+  const int i = min(max((int)fma(m, 128.0, 0.5), kLogBase), kLogBase + kLogTab - 1) - kLogBase;
+  const double u = __dadd_rn(m, -(double)(i + kLogBase) * 0.0078125);
+  const double r = u * lt[2 * kLogTab + i];
+  double q = fma(r, -0.125, 1.0 / 7.0);
+  q = fma(r, q, -1.0 / 6.0);
+  q = fma(r, q, 0.2);
+  q = fma(r, q, -0.25);
+  q = fma(r, q, 1.0 / 3.0);
+  q = fma(r, q, -0.5);
+  const double lp = fma(r * r, q, r);
+  const double ed = (double)e;
+  const double a = __dmul_rn(ed, kLn2Hi);
+  const double h = lt[i];
+  const double sum = __dadd_rn(a, h);
+  const double bb = __dadd_rn(sum, -a);
+  const double err = __dadd_rn(__dadd_rn(a, -__dadd_rn(sum, -bb)), __dadd_rn(h, -bb));
+  const double res = __dadd_rn(sum, lp + (fma(ed, kLn2Lo, lt[kLogTab + i]) + err));
+  return x < __builtin_inf() ? res : x;
+}
+
 __device__ __forceinline__ void ola_store_feature(double acc, int64_t o, float* __restrict__ out,
                                                   double* __restrict__ out64, int16_t* __restrict__ outq,
-                                                  int decimals, double scale10, bool& bad) {
-  const double v = log(acc < 1e-14 ? 1e-14 : acc);  // np.clip(a_min=1e-14) keeps NaN; :227
+                                                  int decimals, double scale10, bool& bad,
+                                                  const double* __restrict__ lt = kLogTable) {
+  const double v = ola_log(acc < 1e-14 ? 1e-14 : acc, lt);  // np.clip(a_min=1e-14) keeps NaN; :227
   if (out64) out64[o] = v;
   const double k = nearbyint(v * scale10);
   if (out) out[o] = decimals >= 0 ? (float)(k / scale10) : (float)v;

@@ -30,6 +30,7 @@ __global__ __launch_bounds__(256) void ola_log_tiled_kernel(DevConsts c, const d
                                                             uint32_t* __restrict__ qflag, int decimals, double scale10) {
   extern __shared__ double tile[];  // [kOlaRows][B + 1]
   __shared__ int fr_lo, fr_hi;      // the frames overlapping the tile
+  __shared__ double ltab[3 * kLogTab];  // ola_log's table
   const int u = blockIdx.y;
   const UttDesc U = utts[u];
   const int t0 = blockIdx.x * kOlaRows;
@@ -38,6 +39,7 @@ __global__ __launch_bounds__(256) void ola_log_tiled_kernel(DevConsts c, const d
   const int B = c.B, BS = c.B + 1, kk = c.kk;
   const int tid = threadIdx.x;
   for (int q = tid; q < kOlaRows * BS; q += blockDim.x) tile[q] = 0.0;
+  for (int q = tid; q < 3 * kLogTab; q += blockDim.x) ltab[q] = kLogTable[q];
   // frames overlapping [t0, t0 + nt): dst is non-decreasing in k, so they are a range; every thread tests
   // its own frames at once (one memory round trip, not a binary search of dependent loads) and the range
   // ends are the smallest / largest frame that overlaps (a frame past t0 + nt or ending before t0 does not)
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(256) void ola_log_tiled_kernel(DevConsts c, const d
     const int t = (int)(((float)q + 0.5f) * invB), j = q - t * B;
     FDLP_CHECK(t >= 0 && t < nt && j >= 0 && j < B);
     ola_store_feature(tile[t * BS + j], (U.out_row + t0 + t) * (int64_t)B + j, out, out64, outq, decimals, scale10,
-                      bad);
+                      bad, ltab);
   }
   if (bad) *qflag = 1u;
 }
@@ -124,6 +126,19 @@ hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc
     (void)hipFuncSetAttribute((const void*)ola_log_tiled_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(ola_log_tiled_kernel, grid, dim3(256), lds, s, c, env, frames, utts, out, out_f64, out_q, q_flag,
                      decimals, scale10);
+  return hipGetLastError();
+}
+
+// the OLA stage's log on n values (fdlp_device_log: accuracy tests of ola_log against numpy)
+__global__ __launch_bounds__(256) void device_log_kernel(const double* __restrict__ x, double* __restrict__ y, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = ola_log(x[i], kLogTable);
+}
+
+hipError_t launch_device_log(const double* x, double* y, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(device_log_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, y, n);
   return hipGetLastError();
 }
 

@@ -1584,6 +1584,13 @@ int fdlp_reverb(const fdlp_reverb_batch* b, void* stream) {
   return FDLP_OK;
 }
 
+int fdlp_device_log(const double* x, double* y, int64_t n, void* stream) {
+  if (n < 0 || (n > 0 && (!x || !y))) return fail(FDLP_E_INVALID, "fdlp_device_log: bad args");
+  const hipError_t e = fdlp::launch_device_log(x, y, n, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(FDLP_E_HIP, std::string("device log kernel: ") + hipGetErrorString(e));
+  return FDLP_OK;
+}
+
 int fdlp_cmvn_accumulate(const float* feats, int64_t rows, int32_t dim, double* stats, void* stream) {
   if (rows < 0 || dim <= 0 || !stats || (rows > 0 && !feats)) return fail(FDLP_E_INVALID, "fdlp_cmvn_accumulate: bad args");
   hipStream_t s = (hipStream_t)stream;
