@@ -748,7 +748,10 @@ __global__ __launch_bounds__(64, 2) void durbin8_kernel(const double* __restrict
 //   dead), the 16 positions a phase adds come from global loads issued one phase ahead.  16 items x 156
 //   doubles = 19.7 KB of LDS per wave, two waves per SIMD.
 // Phases S = 1, 5, 9, ... (odd: the lane strides S and S + 4 with the item stride 156 = -4 mod 32 doubles
-// put the 32 lanes of a ds_read_b64 group and the 16 of a ds_write_b64 group on distinct banks), then SL4.
+// put the 32 lanes of a ds_read_b64 group and the 16 of a ds_write_b64 group on distinct banks), then SL4
+// = 38: the relayout into that last, even phase and its final A image put lanes li and li + 2 of an item
+// on one bank (2-way), 304 extra cycles per wave, ~0.25 % of its time; no item stride avoids it
+// (benchmarks/durbin4_lds_model.py), and an odd SL4 = 39 would cost registers and a larger image.
 // Same recursion and the same kappa / E / 1/E arithmetic as c8_step (features.py:226-228); the order-k dot
 // product is summed over 4 lane partials of 2 chains instead of 8 lanes of 4 chains.
 // -----------------------------------------------------------------------------------------
