@@ -322,11 +322,13 @@ int fdlp_reverb(const fdlp_reverb_batch* batch, void* stream);
 int fdlp_cmvn_accumulate(const float* feats_dev, int64_t rows, int32_t dim, double* stats_dev,
                          void* stream);
 
-/* ---- the OLA stage's device log (for accuracy tests) ---------------------------------------- */
-/* y_dev[i] = the log the OLA stage applies to its clipped sums (computeFDLPSpectrogram.py:227 np.log),
- * for n fp64 values x_dev[i] > 0 (NaN / +inf pass through): a table + polynomial log within ~0.5 ulp
- * (fdlp_device.h ola_log).  ABI 8. */
-int fdlp_device_log(const double* x_dev, double* y_dev, int64_t n, void* stream);
+/* ---- the path's device transcendental functions (for accuracy tests) ------------------------ */
+/* y_dev[i] = fn(x_dev[i]) for n fp64 values on the device, with the function the path itself uses:
+ * FDLP_FN_LOG the OLA stage's log of its clipped sums (computeFDLPSpectrogram.py:227 np.log; x > 0, NaN /
+ * +inf pass through; a table + polynomial form within ~0.5 ulp, fdlp_device.h ola_log), FDLP_FN_EXP the
+ * envelope's exp (:204-205 np.exp; the device library's exp).  ABI 8. */
+enum { FDLP_FN_LOG = 0, FDLP_FN_EXP = 1 };
+int fdlp_device_fn(int32_t fn, const double* x_dev, double* y_dev, int64_t n, void* stream);
 
 /* ---- host-side RNG replicas (no device work) --------------------------------------------- */
 /* CPython `random` (MT19937, init_by_array seeding, randrange(2) = getrandbits(2) with

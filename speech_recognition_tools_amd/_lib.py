@@ -40,6 +40,7 @@ FDLP_WIN_HAMMING = 0
 FDLP_WIN_HANNING = 1
 FDLP_WIN_RECT = 2
 ABI_VERSION = 8
+FDLP_FN_LOG, FDLP_FN_EXP = 0, 1  # fdlp_device_fn
 STAGE_NAMES = ("frames_dft1", "dft2_dct", "autocorr", "lpc_env", "ola_log")
 
 c_i32, c_i64, c_dbl, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
@@ -162,7 +163,7 @@ SIGNATURES = {
     "fdlp_ark_write": (c_i32, [c_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), c_i32, c_i32]),
     "fdlp_ark_close": (c_i32, [c_p]),
     "fdlp_ark_abort": (c_i32, [c_p]),
-    "fdlp_device_log": (c_i32, [c_p, c_p, c_i64, c_p]),
+    "fdlp_device_fn": (c_i32, [c_i32, c_p, c_p, c_i64, c_p]),
     "fdlp_cmvn_accumulate": (c_i32, [c_p, c_i64, c_i32, c_p, c_p]),
     "fdlp_reverb": (c_i32, [ctypes.POINTER(FdlpReverbBatchC), c_p]),
     "fdlp_mel_plan_create": (c_i32, [ctypes.POINTER(FdlpMelConfigC), c_i32, ctypes.POINTER(c_p)]),

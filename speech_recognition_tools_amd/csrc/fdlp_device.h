@@ -8,7 +8,7 @@
 #include <stdint.h>
 
 #include "fdlp_internal.h"
-#include "fdlp_logtab.h"
+#include "fdlp_mathtab.h"
 
 namespace fdlp {
 
@@ -305,7 +305,7 @@ __device__ __forceinline__ int16_t q_code(double k, bool& bad) {
 // log x = e ln2 + log c + log1p(r), log1p(r) by its degree-8 Taylor polynomial (truncation < 1e-19 r);
 // e ln2_hi (exact: 42-bit ln2_hi) + log(c)_hi summed error-free (TwoSum, kept out of FMA contraction by the
 // _rn intrinsics), then the small terms once: within ~0.5 ulp (tests/test_device_log.py: <= 1 ulp against
-// numpy's log over 1e-14 .. 1e12).  NaN and +inf pass through.  lt = kLogTable (fdlp_logtab.h) or a copy
+// numpy's log over 1e-14 .. 1e12).  NaN and +inf pass through.  lt = kLogTable (fdlp_mathtab.h) or a copy
 // of it in LDS.
 __device__ __forceinline__ double ola_log(double x, const double* __restrict__ lt) {
   constexpr double kSqrtHalf = 0.70710678118654752440;

@@ -232,5 +232,5 @@ hipError_t launch_modspec_out(const double* cep, const FrameDesc* frames, const 
                               float* out, double* out64, int decimals, hipStream_t s);
 int cmvn_chunks(int64_t rows);
 hipError_t launch_cmvn(const float* x, int64_t rows, int D, double* part, double* stats, hipStream_t s);
-hipError_t launch_device_log(const double* x, double* y, int64_t n, hipStream_t s);
+hipError_t launch_device_fn(int fn, const double* x, double* y, int64_t n, hipStream_t s);
 }  // namespace fdlp

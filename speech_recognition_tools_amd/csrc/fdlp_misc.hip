@@ -129,16 +129,17 @@ hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc
   return hipGetLastError();
 }
 
-// the OLA stage's log on n values (fdlp_device_log: accuracy tests of ola_log against numpy)
-__global__ __launch_bounds__(256) void device_log_kernel(const double* __restrict__ x, double* __restrict__ y, int64_t n) {
+// the path's log / exp on n values (fdlp_device_fn: accuracy tests of ola_log and the envelope's exp against numpy)
+__global__ __launch_bounds__(256) void device_fn_kernel(int fn, const double* __restrict__ x, double* __restrict__ y,
+                                                        int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    y[i] = ola_log(x[i], kLogTable);
+    y[i] = fn == 0 ? ola_log(x[i], kLogTable) : exp(x[i]);
 }
 
-hipError_t launch_device_log(const double* x, double* y, int64_t n, hipStream_t s) {
+hipError_t launch_device_fn(int fn, const double* x, double* y, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(device_log_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, y, n);
+  hipLaunchKernelGGL(device_fn_kernel, dim3((unsigned)blocks), dim3(256), 0, s, fn, x, y, n);
   return hipGetLastError();
 }
 

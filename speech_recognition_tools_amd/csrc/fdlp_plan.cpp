@@ -1584,10 +1584,11 @@ int fdlp_reverb(const fdlp_reverb_batch* b, void* stream) {
   return FDLP_OK;
 }
 
-int fdlp_device_log(const double* x, double* y, int64_t n, void* stream) {
-  if (n < 0 || (n > 0 && (!x || !y))) return fail(FDLP_E_INVALID, "fdlp_device_log: bad args");
-  const hipError_t e = fdlp::launch_device_log(x, y, n, (hipStream_t)stream);
-  if (e != hipSuccess) return fail(FDLP_E_HIP, std::string("device log kernel: ") + hipGetErrorString(e));
+int fdlp_device_fn(int32_t fn, const double* x, double* y, int64_t n, void* stream) {
+  if ((fn != FDLP_FN_LOG && fn != FDLP_FN_EXP) || n < 0 || (n > 0 && (!x || !y)))
+    return fail(FDLP_E_INVALID, "fdlp_device_fn: bad args");
+  const hipError_t e = fdlp::launch_device_fn(fn, x, y, n, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(FDLP_E_HIP, std::string("device fn kernel: ") + hipGetErrorString(e));
   return FDLP_OK;
 }
 
