@@ -509,6 +509,7 @@ struct Warm {
   fdlp_plan* plan = nullptr;
   hipStream_t s = nullptr, s_in = nullptr, s_out = nullptr;
   std::vector<Slot> slots;
+  std::vector<std::vector<float>> ring;  // the widening stage's buffers (already faulted in)
 };
 std::mutex g_warm_m;
 Warm* g_warm = nullptr;
@@ -677,6 +678,8 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   Warm* warm = take_warm(c, device);
   stats.warm = warm ? 1 : 0;
   std::vector<Slot> slots = warm ? std::move(warm->slots) : std::vector<Slot>(kSlots);
+  std::vector<std::vector<float>> ring = warm && warm->ring.size() == kRing ? std::move(warm->ring)
+                                                                         : std::vector<std::vector<float>>(kRing);
   for (auto& sl : slots) sl.pinned = false;  // usable once the pinning thread has checked (or grown) its buffers
   JobState js;
   // pinning thread: page-locking the slots' host buffers overlaps the plan creation and the first reads;
@@ -743,7 +746,6 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   hipStream_t s_fb = nullptr;  // the float32 copy of a batch whose codes overflowed
   CopyPool copies(4);  // before cleanup(): drained there before the pinned buffers are freed
   PartPool widen_pool(codes ? 5 : 0);
-  std::vector<std::vector<float>> ring(kRing);
   std::string len_text;
   std::thread stage_a, stage_b;
   int32_t sr_seen = -1;  // 'sr' of the last successful read (:139; NameError before the first one)
@@ -797,6 +799,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
         w->s_in = s_in;
         w->s_out = s_out;
         w->slots = std::move(slots);
+        w->ring = std::move(ring);
         Warm* old;
         {
           std::lock_guard<std::mutex> g(g_warm_m);
@@ -989,7 +992,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   } pend;
   int slot_i = 0;
   int64_t n_batch = 0;
-  int32_t ramp = std::max(64, c.max_frames / 8);  // frames of the current batch (see the loop)
+  int32_t ramp = std::max(64, c.max_frames / 32);  // frames of the current batch (see the loop)
 
   // waits until the slot's previous batch is written, then makes it the current one
   auto acquire_slot = [&](int k) -> int {
@@ -1140,7 +1143,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     if (o->progress_name) printf("%s: Computing Features for file: %s\n", o->progress_name, u.id.c_str());  // :185
     // a batch is one PCM kind and at most max_frames frames
     int32_t cap = c.max_frames;
-    // batches ramp up (max_frames / 8, doubling per batch) so the device starts after the first few
+    // batches ramp up (max_frames / 32, at least 64, doubling per batch) so the device starts after the first few
     // reads and the pipeline fill is short; steady state runs at max_frames
     if (!pend.ids.empty() && (pend.frames + F > std::min(cap, ramp) || pend.kind != kind)) {
       JOB_TRY(flush());

@@ -220,7 +220,7 @@ def test_native_and_python_runners_write_identical_arks(tmp_path):
 
 
 def test_native_runner_batch_ramp_matches_python(tmp_path):
-    """300 utterances of 1-6 s through 1024-frame batches: the native runner's ramp (128, 256, 512, 1024
+    """300 utterances of 1-6 s through 1024-frame batches: the native runner's ramp (64, 128, ..., 1024
     frames) and its three-slot rotation write the same bytes as the Python loop."""
     meta, _, _, _ = load_golden("wsj")
     rng = np.random.default_rng(11)
