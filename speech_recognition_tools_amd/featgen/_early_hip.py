@@ -46,10 +46,13 @@ def start(argv):
     if _thread is not None or "torch" in sys.modules:
         return
     from speech_recognition_tools_amd.featgen._fdlp_args import build_parser, narrow_visible_devices, native_eligible
+    import contextlib
+    import io
     try:
-        args, _ = build_parser().parse_known_args(argv)
+        with contextlib.redirect_stderr(io.StringIO()), contextlib.redirect_stdout(io.StringIO()):
+            args, _ = build_parser().parse_known_args(argv)
     except SystemExit:
-        return  # main() prints the usage error
+        return  # -h or a usage error: main() prints it (once)
     try:
         if not native_eligible(args):
             return
