@@ -165,6 +165,26 @@ def pipeline(torch, dev, plans, streams, pcm_h, lens, nj, rng, rows, cfg, kern, 
                 sep = variant.startswith(("stream", "split")) or variant.endswith("s")
                 nso = int(variant[6:]) if variant.startswith("stream") and variant[6:] else 2
                 so = s_out[b % nso] if sep else cs
+                if variant.startswith("hyb"):  # hyb<W>_<P>: the first P % by the copy kernel (W workgroups) on one
+                    # stream, the rest by the runtime's copy (SDMA) on another, both after the batch
+                    w_s, p_s = variant[3:].split("_")
+                    nk = (nqa * int(p_s) // 100) // 8 * 8  # int16 elements, 16-byte pieces for the kernel
+                    es, ee = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    s_k, s_d = s_out[2 + (b % 2)], s_out[b % 2]
+                    for sj in (s_k, s_d):
+                        sj.wait_event(ev_done[i])
+                    es.record(s_d)
+                    if nk > 0:
+                        assert kern.d2h_copy(q_d[i].data_ptr(), mapped(q_h[i]), nk * 2, int(w_s), 1, s_k.cuda_stream) == 0
+                    with torch.cuda.stream(s_d):
+                        q_h[i][nk:].copy_(q_d[i][nk:], non_blocking=True)
+                    ek = torch.cuda.Event()
+                    ek.record(s_k)
+                    s_d.wait_event(ek)
+                    ee.record(s_d)
+                    ev_out[i].record(s_d)
+                    marks.append((es, ee))
+                    continue
                 if variant.startswith("split"):  # each copy in k chunks on k streams
                     k = int(variant[5:])
                     es, ee = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
