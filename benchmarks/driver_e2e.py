@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--jobs-per-gpu", type=int, default=2)
     ap.add_argument("--ngpu", type=int, default=None, help="default: the driver's visible-GPU count")
     ap.add_argument("--keep", default=None, help="write the data dir here instead of a temp dir")
+    ap.add_argument("--trace-dir", default=None, help="the single cold JOB's --job_trace files go here")
     a = ap.parse_args()
     from bench import speech_like
     rs = np.random.RandomState(11)
@@ -91,9 +92,14 @@ def main():
             f.writelines(lines[:max(1, len(lines) // a.nj)])
         cli = os.path.join(ROOT, "speech_recognition_tools_amd", "featgen", "computeFDLPSpectrogram.py")
         one = {}
+        if a.trace_dir:
+            a.trace_dir = os.path.abspath(a.trace_dir)
+            os.makedirs(a.trace_dir, exist_ok=True)
         for k in range(2):
             t1 = time.perf_counter()
-            r1 = subprocess.run(["python3", cli, shard, os.path.join(base, "one_job_%d" % k)] + WSJ_OPTS_CLI + ["--job_stats"],
+            tr = os.path.join(a.trace_dir, "cold_job_%d.jsonl" % k) if a.trace_dir else None
+            r1 = subprocess.run(["python3", cli, shard, os.path.join(base, "one_job_%d" % k)] + WSJ_OPTS_CLI + ["--job_stats"]
+                                + (["--job_trace=" + tr] if tr else []),
                                 cwd=base, capture_output=True, text=True)
             w1 = time.perf_counter() - t1
             if r1.returncode != 0:
