@@ -20,9 +20,11 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
+#include <future>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -255,6 +257,7 @@ class Reader {
     slots_.resize(lines_.size());
     ready_.assign(lines_.size(), 0);
     bytes_.assign(lines_.size(), 0);
+    len_.assign(lines_.size(), -1);
     for (int t = 0; t < std::max(1, threads); ++t) th_.emplace_back([this] { run(); });
   }
   ~Reader() {
@@ -266,6 +269,18 @@ class Reader {
     for (auto& t : th_) t.join();
   }
   size_t size() const { return lines_.size(); }
+  // waits until every entry is read, or `enough` samples are, or `ms` milliseconds have passed; true (and
+  // every entry's sample count, -1 for a failed read, in *lens) if every entry is read
+  bool wait_lengths(int64_t enough, int ms, std::vector<int64_t>* lens) {
+    std::unique_lock<std::mutex> g(m_);
+    ++count_waiters_;
+    cv_count_.wait_for(g, std::chrono::milliseconds(ms),
+                       [&] { return read_n_ >= lines_.size() || read_samples_ >= enough; });
+    --count_waiters_;
+    if (read_n_ < lines_.size()) return false;
+    *lens = len_;
+    return true;
+  }
   // entry i (blocks until read); the caller releases it with done(i)
   Utt& get(size_t i) {
     std::unique_lock<std::mutex> g(m_);
@@ -309,7 +324,9 @@ class Reader {
       Utt u;
       read_entry(lines_[i], u);
       const size_t nb = (u.raw ? u.raw->size() : 0) + (u.f64 ? u.f64->size() * sizeof(double) : 0);
-      bool wake;
+      const bool u_ok = u.ok;
+      const int64_t u_T = u.T, smp = u.ok ? u.T * std::max(1, u.ch) : 0;
+      bool wake, count;
       {
         std::lock_guard<std::mutex> g(m_);
         slots_[i] = std::move(u);
@@ -317,8 +334,13 @@ class Reader {
         ahead_bytes_ += nb;
         ready_[i] = 1;
         wake = want_ == i;
+        ++read_n_;
+        read_samples_ += smp;
+        len_[i] = u_ok ? u_T : -1;
+        count = count_waiters_ > 0;
       }
       if (wake) cv_done_.notify_one();
+      if (count) cv_count_.notify_all();
     }
   }
   std::vector<std::string> lines_;
@@ -331,8 +353,12 @@ class Reader {
   size_t ahead_bytes_ = 0;     // held by entries read and not yet consumed
   int parked_ = 0;          // readers waiting on the depth limit
   bool stop_ = false;
+  size_t read_n_ = 0;          // entries read so far
+  int64_t read_samples_ = 0;   // their samples
+  std::vector<int64_t> len_;   // samples per entry (-1: not read, or the read failed)
+  int count_waiters_ = 0;
   std::mutex m_;
-  std::condition_variable cv_, cv_done_;
+  std::condition_variable cv_, cv_done_, cv_count_;
   std::vector<std::thread> th_;
 };
 
@@ -482,6 +508,41 @@ int grow_device(void** p, size_t* cap, size_t need, hipStream_t s) {
   if (hipMalloc(p, n) != hipSuccess) return fail(FDLP_E_NOMEM, "device allocation failed");
   *cap = n;
   return FDLP_OK;
+}
+
+// The samples and output rows of the largest batch each slot will hold, replaying the main loop's
+// batching over the job's entries (their sample counts from the reader): batches ramp from
+// max(64, max_frames / 32) frames, doubling up to max_frames, hold whole entries, and go round the slots
+// in turn.  Frames and rows per entry are the plan's (fdlp_plan.cpp frames_of / out_of, spectrogram mode).
+void slot_needs(const std::vector<int64_t>& lens, const fdlp_config& c, size_t nslots, std::vector<size_t>* smp,
+                std::vector<size_t>* rows) {
+  const double ov = 1.0 - c.overlap_fraction;
+  const int64_t hop = std::max(1, (int)((double)c.srate / (1.0 / (ov * c.fduration))));
+  const int64_t n = (int64_t)((double)c.srate * c.fduration), d = n % 2 == 0 ? -1 : 0;
+  const int64_t cap = std::max(1, c.max_frames);
+  int64_t ramp = std::max<int64_t>(64, cap / 32), bf = 0, bs = 0, br = 0;
+  size_t j = 0;
+  smp->assign(nslots, 0);
+  rows->assign(nslots, 0);
+  auto put = [&] {
+    (*smp)[j % nslots] = std::max((*smp)[j % nslots], (size_t)bs);
+    (*rows)[j % nslots] = std::max((*rows)[j % nslots], (size_t)br);
+  };
+  for (int64_t T : lens) {
+    const int64_t F = T + d > 0 ? (T + d - 1) / hop + 1 : 0;
+    if (T < 0 || F < 1) continue;
+    const int64_t L = (T * (int64_t)c.frate + c.srate - 1) / std::max(1, c.srate);
+    if (bf && bf + F > std::min(cap, ramp)) {
+      put();
+      ++j;
+      bf = bs = br = 0;
+      ramp = ramp < cap ? 2 * ramp : ramp;
+    }
+    bf += F;
+    bs += T;
+    br += L;
+  }
+  if (bf) put();
 }
 
 void free_slot(Slot& sl) {
@@ -673,7 +734,6 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   const int hop0 = (int)((double)c.srate / (1.0 / (ov * c.fduration)));
   const size_t pin_smp = (size_t)c.max_frames * (size_t)(std::max(hop0, 1) + 1);
   const size_t pin_rows = (size_t)c.max_frames * (size_t)((int64_t)hop0 * c.frate / std::max(1, c.srate) + 2);
-  const size_t pin_dl_bytes = pin_rows * (size_t)std::max(1, c.nfilters) * dl_elem;
 
   Warm* warm = take_warm(c, device);
   stats.warm = warm ? 1 : 0;
@@ -682,9 +742,33 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
                                                                          : std::vector<std::vector<float>>(kRing);
   for (auto& sl : slots) sl.pinned = false;  // usable once the pinning thread has checked (or grown) its buffers
   JobState js;
+  // slot sizes: a full int16 batch, or -- for a cold call whose scp the readers finish within a few ms
+  // (a job smaller than a batch or so) -- what its batches need: pinning and unpinning cost about 0.1 s
+  // per GB, a large part of a short job's process
+  std::vector<size_t> slot_smp(slots.size(), pin_smp), slot_rows(slots.size(), pin_rows);
+  bool sized = false;
+  const bool cold = !warm;
   // pinning thread: page-locking the slots' host buffers overlaps the plan creation and the first reads;
   // slot k becomes usable when slots[k].pinned is set (slots of a warm call are pinned already)
   std::thread pinner([&] {
+    std::vector<size_t> want_smp(slots.size(), pin_smp), want_rows(slots.size(), pin_rows);
+    std::vector<int64_t> lens;
+    if (cold && reader.wait_lengths((int64_t)(pin_smp * slots.size()), 40, &lens)) {
+      std::vector<size_t> ns, nr;
+      slot_needs(lens, c, slots.size(), &ns, &nr);
+      for (size_t k = 0; k < slots.size(); ++k) {
+        want_smp[k] = std::min(pin_smp, ns[k] + ns[k] / 16 + 4096);
+        want_rows[k] = std::min(pin_rows, nr[k] + nr[k] / 16 + 64);
+      }
+    }
+    {
+      std::lock_guard<std::mutex> g(js.m);
+      slot_smp = want_smp;
+      slot_rows = want_rows;
+      sized = true;
+    }
+    js.cv.notify_all();
+    trace.add("sized");
     for (size_t k = 0; k < slots.size(); ++k) {
       const double t0 = now_s();
       void* hp = slots[k].h_pcm;
@@ -692,8 +776,8 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
       void* hd = slots[k].h_dl;
       size_t dcap = slots[k].dl_cap;
       uint32_t* hf = slots[k].h_qflag;
-      int e = grow_pinned(&hp, &pcap, pin_smp * sizeof(int16_t));
-      if (e == FDLP_OK) e = grow_pinned(&hd, &dcap, pin_dl_bytes);
+      int e = grow_pinned(&hp, &pcap, want_smp[k] * sizeof(int16_t));
+      if (e == FDLP_OK) e = grow_pinned(&hd, &dcap, want_rows[k] * (size_t)std::max(1, c.nfilters) * dl_elem);
       if (e == FDLP_OK && !hf && hipHostMalloc((void**)&hf, 64, hipHostMallocDefault) != hipSuccess)
         e = fail(FDLP_E_NOMEM, "pinned host allocation failed");
       std::lock_guard<std::mutex> g(js.m);
@@ -812,9 +896,11 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     }
     if (!parked) {
       for (auto& sl : slots) free_slot(sl);
+      trace.add("slots_freed");
       for (hipStream_t x : {s, s_in, s_out})
         if (x) (void)hipStreamDestroy(x);
       fdlp_plan_destroy(plan);
+      trace.add("plan_freed");
     }
     if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
     stats.seconds = now_s() - t_start;
@@ -1097,11 +1183,15 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     return acquire_slot(slot_i);
   };
 
-  {  // device buffers of a full int16 batch, allocated up front (growth stays possible); the pinned host
-     // buffers come from the pinning thread started before the plan (acquire_slot waits for them)
-    const size_t smp = pin_smp, rows = pin_rows;
+  {  // device buffers of the slot sizes (the pinning thread's), allocated up front (growth stays possible);
+     // the pinned host buffers come from the pinning thread (acquire_slot waits for them)
+    {
+      std::unique_lock<std::mutex> g(js.m);
+      js.cv.wait(g, [&] { return sized || js.pin_err != FDLP_OK; });
+    }
     for (size_t k = 0; k < slots.size(); ++k) {
       Slot& sl = slots[k];
+      const size_t smp = slot_smp[k], rows = slot_rows[k];
       JOB_TRY(grow_device(&sl.d_pcm, &sl.d_pcm_cap, smp * sizeof(int16_t), s));
       if (!mapped || o->cmvn_path) JOB_TRY(grow_device((void**)&sl.d_out, &sl.out_cap, rows * B * sizeof(float), s));
       if (codes) JOB_TRY(grow_device((void**)&sl.d_q, &sl.q_cap, rows * B * sizeof(int16_t), s));
