@@ -920,6 +920,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   if (!s) JOB_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   if (!s_in) JOB_HIP(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking));
   if (!s_out) JOB_HIP(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking));
+  trace.add("streams");
   for (auto& sl : slots) {
     if (!sl.ev_in) JOB_HIP(hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming));
     if (!sl.ev_comp) JOB_HIP(hipEventCreateWithFlags(&sl.ev_comp, hipEventDisableTiming));
@@ -927,6 +928,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
       if (!e) JOB_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (codes && !sl.d_qflag) JOB_HIP(hipMalloc((void**)&sl.d_qflag, 64));
   }
+  trace.add("events");
   JOB_TRY(fdlp_pyrandom_create(o->jitter_key, o->jitter_key_len, &jrng));
   if (o->noise) {
     JOB_TRY(fdlp_nprandom_create(o->noise_seed, &nrng));
@@ -940,6 +942,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   if (codes) JOB_HIP(hipStreamCreateWithFlags(&s_fb, hipStreamNonBlocking));
   const std::string out_s(outfile);
   JOB_TRY(fdlp_ark_open((out_s + ".ark").c_str(), (out_s + ".scp").c_str(), &ark));
+  trace.add("opened");
 
   // stage A (landing + widening): waits for each D2H piece, widens codes into a ring buffer on the part
   // pool (or passes the float32 rows through), and hands the piece to the writer in order
@@ -1116,6 +1119,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     if (hipMemcpyAsync(sl.d_pcm, sl.h_pcm, (size_t)pend.samples * elem, hipMemcpyHostToDevice, s_in) != hipSuccess ||
         hipEventRecord(sl.ev_in, s_in) != hipSuccess || hipStreamWaitEvent(s, sl.ev_in, 0) != hipSuccess)
       return fail(FDLP_E_HIP, "H2D copy failed");
+    trace.add("h2d", n_batch);
     fdlp_batch b{};
     b.n_utt = (int32_t)pend.ids.size();
     b.pcm_kind = pend.kind;
@@ -1138,6 +1142,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
       return fail(FDLP_E_HIP, "flag reset failed");
     r = fdlp_compute(plan, &b, s);
     if (r != FDLP_OK) return r;
+    trace.add("computed", n_batch);
     if (d_cmvn) {
       r = fdlp_cmvn_accumulate(sl.d_out, pend.out_rows, B, d_cmvn, s);
       if (r != FDLP_OK) return r;
@@ -1189,6 +1194,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
       std::unique_lock<std::mutex> g(js.m);
       js.cv.wait(g, [&] { return sized || js.pin_err != FDLP_OK; });
     }
+    trace.add("alloc");
     for (size_t k = 0; k < slots.size(); ++k) {
       Slot& sl = slots[k];
       const size_t smp = slot_smp[k], rows = slot_rows[k];
