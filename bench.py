@@ -473,9 +473,10 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
     rows, D = out.shape
     nq = rows * D
     pin_in = torch.from_numpy(pcm_host).pin_memory()
-    NB = 2 * B                                       # device buffer sets: (batch, step parity)
-    pcm_d = [pcms[i // 2] if i % 2 == 0 else torch.empty_like(pcms[0]) for i in range(NB)]
-    out_d = [outs[i // 2] if i % 2 == 0 else torch.empty_like(out) for i in range(NB)]
+    S = max(1, args.xfer_sets)                       # device buffer sets per batch, used in turn
+    NB = S * B                                       # (batch, step mod S)
+    pcm_d = [pcms[i // S] if i % S == 0 else torch.empty_like(pcms[0]) for i in range(NB)]
+    out_d = [outs[i // S] if i % S == 0 else torch.empty_like(out) for i in range(NB)]
     # codes + the flag word in one buffer: [nq int16 codes | int32 flag], one D2H copy per batch
     q_d = [torch.empty(nq + 2, dtype=torch.int16, device=dev) for _ in range(NB)]
     q_h = [torch.empty(nq + 2, dtype=torch.int16).pin_memory() for _ in range(NB)]
@@ -489,8 +490,8 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
     ev_done = [torch.cuda.Event() for _ in range(NB)]
     ev_out = [torch.cuda.Event() for _ in range(NB)]
     for i in range(NB):
-        ev_done[i].record(comp[(i // 2) % len(comp)])
-        ev_out[i].record(comp[(i // 2) % len(comp)])
+        ev_done[i].record(comp[(i // S) % len(comp)])
+        ev_out[i].record(comp[(i // S) % len(comp)])
     it = [0]
     mode = ["codes"]
 
@@ -525,17 +526,17 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
             ev_out[i].record(so)
 
     def xstep():
-        par = it[0] & 1
+        par = it[0] % S
         it[0] += 1
         for b in range(B):
-            xbatch(b, 2 * b + par)
+            xbatch(b, S * b + par)
 
     cpu_dev = torch.device("cpu")
     from speech_recognition_tools_amd.shard import timed_steps
     el_x = timed_steps(xstep, args.steps, args.warmup, sync, dd, cpu_dev)
     flags = [int(q[nq:].view(torch.int32)[0]) for q in q_h]
     # the codes of the last steps' batches widen to the float32 rows still in HBM (bit-identical)
-    par = (it[0] - 1) & 1
+    par = (it[0] - 1) % S
     wid = q_widen(q_h[par][:nq], 3, threads=16).reshape(rows, D)
     same = bool(np.array_equal(wid.view(np.uint32), out_d[par].cpu().numpy().view(np.uint32)))
     t0 = time.perf_counter()
@@ -562,9 +563,9 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
             "mapped_codes": variant("mapped", {"note": "the OLA kernel stores the codes straight into pinned host "
                                                        "memory (fdlp_mapped_ptr) instead of a D2H copy"}),
             "note": "every batch's PCM copied in from pinned host memory and its compact feature codes copied "
-                    "back every step (%d batch(es) in flight on %d compute stream(s), two device buffer sets per "
-                    "batch on alternate steps, one H2D stream, %d D2H stream(s)); not the headline (inputs "
-                    "resident in HBM)" % (B, len(comp), nd)}
+                    "back every step (%d batch(es) in flight on %d compute stream(s), %d device buffer sets per "
+                    "batch used in turn, one H2D stream, %d D2H stream(s)); not the headline (inputs "
+                    "resident in HBM)" % (B, len(comp), S, nd)}
 
 
 def parse_args(argv=None):
@@ -593,6 +594,9 @@ def parse_args(argv=None):
                     help="PCIe pass: the variants timed after the compact-code pass (float32 D2H, mapped codes)")
     ap.add_argument("--xfer-only", action="store_true", help=argparse.SUPPRESS)  # the PCIe-pass child
     ap.add_argument("--xfer-shard", default=None, help=argparse.SUPPRESS)  # rank/world of the child's shard
+    ap.add_argument("--xfer-sets", type=int, default=2,
+                    help="PCIe pass: device buffer sets per batch in flight, used in turn (2: step s + 1's copy-in "
+                         "overlaps step s's kernels and step s - 1's copy-out)")
     ap.add_argument("--xfer-compute-streams", type=int, default=0,
                     help="PCIe pass: compute streams for the batches in flight (0: one per batch)")
     ap.add_argument("--pipeline", type=int, default=None, help="sub-batches over two streams (plan default 1)")

@@ -117,7 +117,10 @@ def main():
 def pipeline(torch, dev, plans, streams, pcm_h, lens, nj, rng, rows, cfg, kern, mapped, steps=10):
     """bench.py's PCIe pass (codes) with per-copy HIP events: where does the D2H go slow?  Variants of where
     the D2H is issued: 'stream' (bench: its own stream after an event wait), 'compute' (on the compute
-    stream right after the batch), 'kernel64' (the copy kernel on the compute stream, 64 workgroups)."""
+    stream right after the batch), 'kernel64' (the copy kernel on the compute stream, 64 workgroups).
+    A prefix 'h2dk<W>+' issues the host-to-device PCM copy as the copy kernel with W workgroups reading the
+    pinned host buffer through its device mapping (on the H2D stream), so it leaves the SDMA engines to the
+    device-to-host leg; 'h2dk<W>+none' is that H2D with no D2H."""
     import time
     K = len(plans)
     nq = rows * cfg.nfilters
@@ -141,6 +144,11 @@ def pipeline(torch, dev, plans, streams, pcm_h, lens, nj, rng, rows, cfg, kern, 
         marks = []
         it = [0]
 
+        h2d, variant = variant.split("+", 1) if "+" in variant else ("", variant)
+        h2d_wgs = int(h2d[4:]) if h2d.startswith("h2dk") else 0
+        pcm_bytes = pcm_h.numel() * pcm_h.element_size()
+        assert pcm_bytes % 16 == 0
+
         def xstep():
             par = it[0] & 1
             it[0] += 1
@@ -149,7 +157,11 @@ def pipeline(torch, dev, plans, streams, pcm_h, lens, nj, rng, rows, cfg, kern, 
                 cs = streams[b]
                 s_in.wait_event(ev_done[i])
                 with torch.cuda.stream(s_in):
-                    pcm_d[i].copy_(pcm_h, non_blocking=True)
+                    if h2d_wgs:
+                        assert kern.d2h_copy(mapped(pcm_h), pcm_d[i].data_ptr(), pcm_bytes, h2d_wgs, 1,
+                                             s_in.cuda_stream) == 0
+                    else:
+                        pcm_d[i].copy_(pcm_h, non_blocking=True)
                     ev_in[i].record(s_in)
                 cs.wait_event(ev_in[i])
                 cs.wait_event(ev_out[i])
@@ -233,7 +245,9 @@ def pipeline(torch, dev, plans, streams, pcm_h, lens, nj, rng, rows, cfg, kern, 
         torch.cuda.synchronize(dev)
         el = time.perf_counter() - t0
         ms = sorted(a.elapsed_time(b) for a, b in marks) or [0.0]
-        print(json.dumps(dict(variant=variant, audio_h_per_s=round(steps * K * audio_h / el, 1),
+        if h2d_wgs:
+            assert torch.equal(pcm_d[0].cpu(), pcm_h)
+        print(json.dumps(dict(variant=(h2d + "+" if h2d else "") + variant, audio_h_per_s=round(steps * K * audio_h / el, 1),
                               ms_per_step=round(el / steps * 1e3, 2), d2h_ms_median=round(ms[len(ms) // 2], 3),
                               d2h_ms_max=round(ms[-1], 3), d2h_GBps_median=round(nq * 2 / max(ms[len(ms) // 2], 1e-6) / 1e6, 1))),
               flush=True)
