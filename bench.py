@@ -473,7 +473,8 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
     rows, D = out.shape
     nq = rows * D
     pin_in = torch.from_numpy(pcm_host).pin_memory()
-    S = max(1, args.xfer_sets)                       # device buffer sets per batch, used in turn
+    grouped = args.xfer_schedule == "grouped"
+    S = max(3 if grouped else 1, args.xfer_sets)     # device buffer sets per batch, used in turn
     NB = S * B                                       # (batch, step mod S)
     pcm_d = [pcms[i // S] if i % S == 0 else torch.empty_like(pcms[0]) for i in range(NB)]
     out_d = [outs[i // S] if i % S == 0 else torch.empty_like(out) for i in range(NB)]
@@ -495,12 +496,26 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
     it = [0]
     mode = ["codes"]
 
-    def xbatch(b, i):
-        cs = comp[b % len(comp)]
+    def copy_in(i):
         s_in.wait_event(ev_done[i])                  # pcm_d[i] no longer read by its previous compute
         with torch.cuda.stream(s_in):
             pcm_d[i].copy_(pin_in, non_blocking=True)
             ev_in[i].record(s_in)
+
+    def copy_out(b, i):
+        so = s_in if grouped else s_outs[b % nd]
+        so.wait_event(ev_done[i])
+        with torch.cuda.stream(so):
+            if mode[0] == "float32":
+                out_h[i].copy_(out_d[i], non_blocking=True)
+            else:
+                q_h[i].copy_(q_d[i], non_blocking=True)
+            ev_out[i].record(so)
+
+    def xbatch(b, i, h2d=True, d2h=True):
+        cs = comp[b % len(comp)]
+        if h2d:
+            copy_in(i)
         cs.wait_event(ev_in[i])
         cs.wait_event(ev_out[i])                     # out_d[i] / q_d[i] copied out by its previous D2H
         with torch.cuda.stream(cs):
@@ -516,20 +531,28 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
         if mode[0] == "mapped":
             ev_out[i].record(cs)
             return
-        so = s_outs[b % nd]
-        so.wait_event(ev_done[i])
-        with torch.cuda.stream(so):
-            if mode[0] == "float32":
-                out_h[i].copy_(out_d[i], non_blocking=True)
-            else:
-                q_h[i].copy_(q_d[i], non_blocking=True)
-            ev_out[i].record(so)
+        if d2h:
+            copy_out(b, i)
 
     def xstep():
         par = it[0] % S
         it[0] += 1
+        if not grouped:
+            for b in range(B):
+                xbatch(b, S * b + par)
+            return
+        # grouped: one copy stream carries step k + 1's copy-ins, then step k's copy-outs, so an H2D never
+        # overlaps a D2H (together they slow the D2H to a fifth of its rate, profiles/r05a_xfer_codes_timeline.txt)
+        if it[0] == 1:
+            for b in range(B):
+                copy_in(S * b + par)
         for b in range(B):
-            xbatch(b, S * b + par)
+            copy_in(S * b + (par + 1) % S)
+        for b in range(B):
+            xbatch(b, S * b + par, h2d=False, d2h=False)
+        if mode[0] != "mapped":
+            for b in range(B):
+                copy_out(b, S * b + par)
 
     cpu_dev = torch.device("cpu")
     from speech_recognition_tools_amd.shard import timed_steps
@@ -597,6 +620,9 @@ def parse_args(argv=None):
     ap.add_argument("--xfer-sets", type=int, default=2,
                     help="PCIe pass: device buffer sets per batch in flight, used in turn (2: step s + 1's copy-in "
                          "overlaps step s's kernels and step s - 1's copy-out)")
+    ap.add_argument("--xfer-schedule", default="streams", choices=["streams", "grouped"],
+                    help="PCIe pass: streams = copy-ins on one stream, copy-outs on --xfer-d2h-streams others; "
+                         "grouped = one copy stream, each step's next copy-ins then its copy-outs (3+ buffer sets)")
     ap.add_argument("--xfer-compute-streams", type=int, default=0,
                     help="PCIe pass: compute streams for the batches in flight (0: one per batch)")
     ap.add_argument("--pipeline", type=int, default=None, help="sub-batches over two streams (plan default 1)")
