@@ -482,7 +482,8 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
     q_d = [torch.empty(nq + 2, dtype=torch.int16, device=dev) for _ in range(NB)]
     q_h = [torch.empty(nq + 2, dtype=torch.int16).pin_memory() for _ in range(NB)]
     out_h = [torch.empty(out.shape, dtype=out.dtype).pin_memory() for _ in range(NB)]
-    s_in = torch.cuda.Stream(dev)
+    s_ins = [torch.cuda.Stream(dev) for _ in range(max(1, args.xfer_h2d_streams))]
+    s_in = s_ins[0]
     nd = args.xfer_d2h_streams or (2 if args.xfer_only else 1)
     s_outs = [torch.cuda.Stream(dev) for _ in range(nd)]
     nc = args.xfer_compute_streams or B
@@ -497,10 +498,11 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
     mode = ["codes"]
 
     def copy_in(i):
-        s_in.wait_event(ev_done[i])                  # pcm_d[i] no longer read by its previous compute
-        with torch.cuda.stream(s_in):
+        si = s_in if grouped else s_ins[(i // S) % len(s_ins)]
+        si.wait_event(ev_done[i])                    # pcm_d[i] no longer read by its previous compute
+        with torch.cuda.stream(si):
             pcm_d[i].copy_(pin_in, non_blocking=True)
-            ev_in[i].record(s_in)
+            ev_in[i].record(si)
 
     def copy_out(b, i):
         so = s_in if grouped else s_outs[b % nd]
@@ -512,20 +514,21 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
                 q_h[i].copy_(q_d[i], non_blocking=True)
             ev_out[i].record(so)
 
-    def xbatch(b, i, h2d=True, d2h=True):
+    def xbatch(b, i, h2d=True, d2h=True, jit=None):
         cs = comp[b % len(comp)]
+        jit = rng.randbits2(nj) if jit is None else jit
         if h2d:
             copy_in(i)
         cs.wait_event(ev_in[i])
         cs.wait_event(ev_out[i])                     # out_d[i] / q_d[i] copied out by its previous D2H
         with torch.cuda.stream(cs):
             if mode[0] == "float32":
-                plans[b].compute(pcm_d[i], lens, rng.randbits2(nj), out=out_d[i], **mix[b])
+                plans[b].compute(pcm_d[i], lens, jit, out=out_d[i], **mix[b])
             else:
                 qt = q_h[i] if mode[0] == "mapped" else q_d[i]
                 flag = qt[nq:].view(torch.int32)
                 flag.zero_()
-                plans[b].compute(pcm_d[i], lens, rng.randbits2(nj), out=out_d[i], out_q=qt[:nq].view(rows, D),
+                plans[b].compute(pcm_d[i], lens, jit, out=out_d[i], out_q=qt[:nq].view(rows, D),
                                  q_flag=flag, **mix[b])
             ev_done[i].record(cs)
         if mode[0] == "mapped":
@@ -534,9 +537,21 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
         if d2h:
             copy_out(b, i)
 
+    nth = max(1, min(args.xfer_threads, B))
+    pool = None
+    if nth > 1:  # host threads issuing the batches (b = t, t + nth, ...); the jitter is drawn here, in order
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(nth)
+
     def xstep():
         par = it[0] % S
         it[0] += 1
+        if pool is not None and not grouped:
+            jits = [rng.randbits2(nj) for _ in range(B)]
+            run = lambda t: [xbatch(b, S * b + par, jit=jits[b]) for b in range(t, B, nth)]
+            for fu in [pool.submit(run, t) for t in range(nth)]:
+                fu.result()
+            return
         if not grouped:
             for b in range(B):
                 xbatch(b, S * b + par)
@@ -623,6 +638,10 @@ def parse_args(argv=None):
     ap.add_argument("--xfer-schedule", default="streams", choices=["streams", "grouped"],
                     help="PCIe pass: streams = copy-ins on one stream, copy-outs on --xfer-d2h-streams others; "
                          "grouped = one copy stream, each step's next copy-ins then its copy-outs (3+ buffer sets)")
+    ap.add_argument("--xfer-h2d-streams", type=int, default=1,
+                    help="PCIe pass: host-to-device copy streams (batch b on stream b mod n)")
+    ap.add_argument("--xfer-threads", type=int, default=1,
+                    help="PCIe pass: host threads issuing the batches' copies and kernels (batch b on thread b mod T)")
     ap.add_argument("--xfer-compute-streams", type=int, default=0,
                     help="PCIe pass: compute streams for the batches in flight (0: one per batch)")
     ap.add_argument("--pipeline", type=int, default=None, help="sub-batches over two streams (plan default 1)")
