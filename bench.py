@@ -363,11 +363,18 @@ RANK_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR
             "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID")
 
 
-def xfer_child_spec(args, world, rank, local, argv=None, environ=None):
+def child_inflight(args):
+    """batches in flight of each --xfer-procs child: --xfer-child-inflight, or the rank's share of --inflight"""
+    return args.xfer_child_inflight or max(1, args.inflight // max(1, args.xfer_procs))
+
+
+def xfer_child_spec(args, world, rank, local, argv=None, environ=None, j=0, procs=1):
     """argv and environment of the PCIe-pass child of one rank (started before the rank touches the GPU):
     a single-process bench.py --xfer-only over the rank's own shard (--xfer-shard rank/world), on the rank's
     GPU only (HIP_VISIBLE_DEVICES narrowed to it), with GPU_MAX_HW_QUEUES = --xfer-hw-queues (read once per
-    process, so the rank's own timed steps keep the default), and no rendezvous variables."""
+    process, so the rank's own timed steps keep the default), and no rendezvous variables.
+    procs > 1: child j of the rank's `procs` takes shard rank * procs + j of world * procs, 1/procs of the
+    batches in flight, and meets its siblings at a start barrier (--xfer-barrier)."""
     argv = list(sys.argv[1:] if argv is None else argv)
     environ = os.environ if environ is None else environ
     out, skip = [], False
@@ -383,7 +390,10 @@ def xfer_child_spec(args, world, rank, local, argv=None, environ=None):
         if a.startswith("--gpus=") or a.startswith("--xfer-shard="):
             continue
         out.append(a)
-    out += ["--xfer-only", "--no-cpu-baseline", "--gpus", "1", "--xfer-shard", "%d/%d" % (rank, world)]
+    out += ["--xfer-only", "--no-cpu-baseline", "--gpus", "1",
+            "--xfer-shard", "%d/%d" % (rank * procs + j, world * procs)]
+    if procs > 1:
+        out += ["--inflight", str(child_inflight(args)), "--xfer-variants", "", "--xfer-barrier"]
     env = {k: v for k, v in environ.items() if k not in RANK_ENV}
     env["GPU_MAX_HW_QUEUES"] = str(args.xfer_hw_queues)
     if world > 1:
@@ -397,26 +407,107 @@ def xfer_child_spec(args, world, rank, local, argv=None, environ=None):
 
 
 def combine_xfer_children(got):
-    """The ranks' PCIe-pass children -> one with_transfers block: total audio over the slowest child (the
-    children run concurrently, one per GPU, but without a shared barrier); None if any child failed."""
+    """The ranks' PCIe-pass children -> one with_transfers block: total audio over the union of their timed
+    regions, first start to last end on absolute clocks (the children run concurrently, one per GPU, but
+    without a shared barrier, so a child that starts late lengthens the wall instead of hiding in a max of
+    per-child times); None if any child failed."""
     if any(g is None or "audio_h" not in g for g in got):
         return None
     x = dict(got[0])
-    x["value"] = sum(g["audio_h"] for g in got) / max(g["elapsed_s"] for g in got)
-    x["ms_per_step"] = max(g["ms_per_step"] for g in got)
+    if all("t_go" in g for g in got):
+        t0 = min(g["t_go"] for g in got)
+        wall = max(g["t_go"] + g["elapsed_s"] for g in got) - t0
+        x["start_spread_s"] = max(g["t_go"] for g in got) - t0
+    else:
+        wall = max(g["elapsed_s"] for g in got)
+    x["value"] = sum(g["audio_h"] for g in got) / wall
+    steps = max(1, round(got[0]["elapsed_s"] * 1e3 / got[0]["ms_per_step"]))
+    x["ms_per_step"] = wall / steps * 1e3
     x["audio_h"] = sum(g["audio_h"] for g in got)
-    x["elapsed_s"] = max(g["elapsed_s"] for g in got)
+    x["elapsed_s"] = wall
     x["per_rank_value"] = [g["value"] for g in got]
-    for k in ("float32_d2h", "mapped_codes"):
+    for k in ("float32_d2h", "mapped_codes", "t_go"):
         x.pop(k, None)
     x["note"] = (x.get("note", "") + "; one child process per rank on its own GPU, started before the rank "
-                 "touches it, all at once: value = total audio / the slowest child's time")
+                 "touches it, all at once: value = total audio / first start to last end")
+    return x
+
+
+def run_xfer_children(args, world=1, rank=0, local=0):
+    """--xfer-procs P > 1: P PCIe-pass children of this rank on its GPU at once (as the recipe runs several
+    JOBs per GPU), each over its shard with 1/P of the batches in flight.  Every child reports when its
+    warmup is done and waits; all are released together, and value = their total audio over the union of
+    their timed regions (first start to last end, absolute clocks).  None if any child fails."""
+    import tempfile
+    P = args.xfer_procs
+    procs, errs = [], []
+    for j in range(P):
+        argv, env = xfer_child_spec(args, world, rank, local, j=j, procs=P)
+        err = tempfile.TemporaryFile(mode="w+")
+        errs.append(err)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, text=True,
+                                      stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=err))
+    ok = True
+    for p in procs:  # each child's READY line (after its warmup)
+        while True:
+            line = p.stdout.readline()
+            if not line or line.strip() == "XFER_READY":
+                ok = ok and bool(line)
+                break
+    got = []
+    for p in procs:
+        try:
+            if ok:
+                p.stdin.write("go\n")
+            p.stdin.close()
+        except OSError:
+            ok = False
+    for p, err in zip(procs, errs):
+        out = p.stdout.read()  # stdin is closed and stderr goes to a file: one pipe, no deadlock
+        try:
+            p.wait(timeout=900)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+            ok = False
+        lines = [l for l in (out or "").strip().splitlines() if l.startswith("{")]
+        if p.returncode != 0 or not lines:
+            err.seek(0)
+            print("bench.py: PCIe-pass child failed (rc %s):\n%s" % (p.returncode, err.read()[-2000:]), file=sys.stderr)
+            ok = False
+        else:
+            got.append(json.loads(lines[-1])["with_transfers"])
+        err.close()
+    if not ok or len(got) != P:
+        return None
+    t0 = min(g["t_go"] for g in got)
+    t1 = max(g["t_go"] + g["elapsed_s"] for g in got)
+    x = dict(got[0])
+    x["audio_h"] = sum(g["audio_h"] for g in got)
+    x["elapsed_s"] = t1 - t0
+    x["value"] = x["audio_h"] / x["elapsed_s"]
+    x["ms_per_step"] = x["elapsed_s"] / args.steps * 1e3
+    x["h2d_bytes_per_step"] = sum(g["h2d_bytes_per_step"] for g in got)
+    x["d2h_bytes_per_step"] = sum(g["d2h_bytes_per_step"] for g in got)
+    x["codes_flagged_batches"] = sum(g["codes_flagged_batches"] for g in got)
+    x["codes_widen_bit_identical"] = all(g["codes_widen_bit_identical"] for g in got)
+    x["per_process_value"] = [g["value"] for g in got]
+    x["start_spread_s"] = max(g["t_go"] for g in got) - t0
+    x["processes_per_gpu"] = P
+    for k in ("float32_d2h", "mapped_codes", "t_go"):
+        x.pop(k, None)
+    x["note"] = ("%d processes on the GPU at once (the recipe runs several JOBs per GPU), each over its own "
+                 "utterances with %d batches in flight (the headline: %d), released together after their warmups: value "
+                 "= their total audio / first start to last end; per process: %s" %
+                 (P, child_inflight(args), args.inflight, got[0].get("note", "")))
     return x
 
 
 def run_xfer_child(args, world=1, rank=0, local=0):
     """bench.py --xfer-only in a child process (xfer_child_spec); its with_transfers block, or None (with
     the child's tail on stderr) when it fails."""
+    if args.xfer_procs > 1:
+        return run_xfer_children(args, world, rank, local)
     argv, env = xfer_child_spec(args, world, rank, local)
     try:
         p = subprocess.run([sys.executable, os.path.abspath(__file__)] + argv, env=env, capture_output=True,
@@ -571,7 +662,14 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
 
     cpu_dev = torch.device("cpu")
     from speech_recognition_tools_amd.shard import timed_steps
-    el_x = timed_steps(xstep, args.steps, args.warmup, sync, dd, cpu_dev)
+    t_go = [time.time()]
+
+    def start_barrier():  # --xfer-barrier: the parent releases its PCIe-pass children together
+        if args.xfer_barrier:
+            print("XFER_READY", flush=True)
+            sys.stdin.readline()
+        t_go[0] = time.time()  # absolute start of the timed region (children combine on the union)
+    el_x = timed_steps(xstep, args.steps, args.warmup, sync, dd, cpu_dev, before_timed=start_barrier)
     flags = [int(q[nq:].view(torch.int32)[0]) for q in q_h]
     # the codes of the last steps' batches widen to the float32 rows still in HBM (bit-identical)
     par = (it[0] - 1) % S
@@ -589,6 +687,7 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
             el_v[v] = timed_steps(xstep, args.steps, 1, sync, dd, cpu_dev)
     variant = lambda v, d: dict(value=ah / el_v[v], ms_per_step=el_v[v] / args.steps * 1e3, **d) if v in el_v else None
     return {"value": ah / el_x, "ms_per_step": el_x / args.steps * 1e3, "audio_h": ah, "elapsed_s": el_x,
+            "t_go": t_go[0],
             "h2d_bytes_per_step": int(B * pcm_host.nbytes), "d2h_bytes_per_step": int(B * (nq + 2) * 2),
             "d2h_encoding": "compact ark codes: int16 nearbyint(v * 1e3) + an int32 flag per batch (ABI 7)",
             "codes_flagged_batches": sum(1 for f in flags if f), "codes_widen_bit_identical": same,
@@ -638,6 +737,12 @@ def parse_args(argv=None):
     ap.add_argument("--xfer-schedule", default="streams", choices=["streams", "grouped"],
                     help="PCIe pass: streams = copy-ins on one stream, copy-outs on --xfer-d2h-streams others; "
                          "grouped = one copy stream, each step's next copy-ins then its copy-outs (3+ buffer sets)")
+    ap.add_argument("--xfer-procs", type=int, default=1,
+                    help="PCIe pass: child processes on each GPU at once, each with 1/P of the batches in flight "
+                         "over its own utterances (the recipe runs several JOBs per GPU)")
+    ap.add_argument("--xfer-child-inflight", type=int, default=0,
+                    help="PCIe pass with --xfer-procs: batches in flight per process (0: --inflight / P)")
+    ap.add_argument("--xfer-barrier", action="store_true", help=argparse.SUPPRESS)  # child of --xfer-procs > 1
     ap.add_argument("--xfer-h2d-streams", type=int, default=1,
                     help="PCIe pass: host-to-device copy streams (batch b on stream b mod n)")
     ap.add_argument("--xfer-threads", type=int, default=1,

@@ -71,6 +71,25 @@ def test_pcie_children_combine():
     x = b.combine_xfer_children(got)
     assert abs(x["value"] - 16.0) < 1e-12 and x["ms_per_step"] == 12.5 and x["per_rank_value"] == [10.0, 8.0]
     assert b.combine_xfer_children([got[0], None]) is None
+    # with the children's absolute start times: the union of their timed regions (a late start lengthens it)
+    got[0]["t_go"], got[1]["t_go"] = 100.0, 100.05
+    x = b.combine_xfer_children(got)
+    assert abs(x["elapsed_s"] - 0.175) < 1e-9 and abs(x["value"] - 2.0 / 0.175) < 1e-9
+    assert abs(x["start_spread_s"] - 0.05) < 1e-9 and abs(x["ms_per_step"] - 17.5) < 1e-9 and "t_go" not in x
+
+
+def test_pcie_children_per_gpu_spec():
+    """--xfer-procs P: child j of rank r takes shard r P + j of W P, 1/P of the batches, and the start barrier"""
+    b = _bench_module()
+    args = b.parse_args(["--xfer-procs", "2", "--inflight", "4"])
+    for j in range(2):
+        a, env = b.xfer_child_spec(args, 2, 1, 1, argv=["--xfer-procs", "2", "--inflight", "4"], environ={}, j=j,
+                                   procs=2)
+        assert a[a.index("--xfer-shard") + 1] == "%d/4" % (2 + j)
+        assert a[len(a) - 1 - a[::-1].index("--inflight") + 1] == "2" and "--xfer-barrier" in a
+        assert a[a.index("--xfer-variants") + 1] == "" and env["HIP_VISIBLE_DEVICES"] == "1"
+    a, _ = b.xfer_child_spec(args, 1, 0, 0, argv=[], environ={})
+    assert "--xfer-barrier" not in a and a[a.index("--xfer-shard") + 1] == "0/1"
 
 
 def _bench_module():
