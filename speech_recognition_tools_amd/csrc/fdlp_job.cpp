@@ -742,7 +742,7 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
                                                                          : std::vector<std::vector<float>>(kRing);
   for (auto& sl : slots) sl.pinned = false;  // usable once the pinning thread has checked (or grown) its buffers
   JobState js;
-  // slot sizes: a full int16 batch, or -- for a cold call whose scp the readers finish within a few ms
+  // slot sizes: a full int16 batch, or -- for a cold call whose scp the readers finish within 10 ms
   // (a job smaller than a batch or so) -- what its batches need: pinning and unpinning cost about 0.1 s
   // per GB, a large part of a short job's process
   std::vector<size_t> slot_smp(slots.size(), pin_smp), slot_rows(slots.size(), pin_rows);
@@ -753,7 +753,10 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   std::thread pinner([&] {
     std::vector<size_t> want_smp(slots.size(), pin_smp), want_rows(slots.size(), pin_rows);
     std::vector<int64_t> lens;
-    if (cold && reader.wait_lengths((int64_t)(pin_smp * slots.size()), 40, &lens)) {
+    // (a job that has read a full batch of samples already gets full-size slots: no wait beyond that; a
+    // scp of more than kSizeLines entries is taken as large without waiting, so its pinning starts at once)
+    constexpr size_t kSizeLines = 4096;
+    if (cold && reader.size() <= kSizeLines && reader.wait_lengths((int64_t)pin_smp, 10, &lens)) {
       std::vector<size_t> ns, nr;
       slot_needs(lens, c, slots.size(), &ns, &nr);
       for (size_t k = 0; k < slots.size(); ++k) {
