@@ -811,13 +811,42 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   if (c.lifter) key_lifter.assign(c.lifter, c.lifter + c.coeff_num);
   delete warm;
   warm = nullptr;
+  // a cold call creates its streams on a helper thread while the plan is built, and moves a few MB each way
+  // on them once: the first large copy of a stream sets up its DMA queue (~7-8 ms), off the first batches' path
+  hipError_t stream_err = hipSuccess;
+  std::thread streamer;
+  if (cold)
+    streamer = std::thread([&] {
+      stream_err = hipSetDevice(device);
+      for (hipStream_t* x : {&s, &s_in, &s_out})
+        if (!*x && stream_err == hipSuccess) stream_err = hipStreamCreateWithFlags(x, hipStreamNonBlocking);
+      if (stream_err != hipSuccess) return;
+      constexpr size_t kWarmBytes = size_t(4) << 20;
+      void *hb = nullptr, *db = nullptr;
+      if (hipHostMalloc(&hb, kWarmBytes, hipHostMallocDefault) == hipSuccess && hipMalloc(&db, kWarmBytes) == hipSuccess) {
+        for (hipStream_t x : {s_in, s}) {
+          (void)hipMemcpyAsync(db, hb, kWarmBytes, hipMemcpyHostToDevice, x);
+          (void)hipStreamSynchronize(x);
+        }
+        (void)hipMemcpyAsync(hb, db, kWarmBytes, hipMemcpyDeviceToHost, s_out);
+        (void)hipStreamSynchronize(s_out);
+      }
+      if (db) (void)hipFree(db);
+      if (hb) (void)hipHostFree(hb);
+      trace.add("streams_warm");
+    });
   const double t_plan = now_s();
   int rc = plan ? FDLP_OK : fdlp_plan_create(&c, device, &plan);
   stats.plan_seconds = now_s() - t_plan;
+  if (streamer.joinable()) streamer.join();
   trace.add("plan");
+  if (rc == FDLP_OK && stream_err != hipSuccess)
+    rc = fail(FDLP_E_HIP, std::string("stream setup: ") + hipGetErrorString(stream_err));
   if (rc != FDLP_OK) {
     join_pinner();
     for (auto& sl : slots) free_slot(sl);
+    for (hipStream_t x : {s, s_in, s_out})
+      if (x) (void)hipStreamDestroy(x);
     return rc;
   }
   int32_t B = 0;
