@@ -224,8 +224,8 @@ STAGE_KERNELS = {"dct": ("fdlp::dct_frame", "fdlp::frames_dft1", "fdlp::dft2_dct
                  "autocorr": {"structured": ("fdlp::ac_vsweep_kernel", "fdlp::ac_wrap_kernel", "fdlp::ac_band_kernel"),
                               "structured_mfma": ("fdlp::ac_sweep_kernel", "fdlp::ac_band_kernel"),
                               "direct": ("fdlp::autocorr_kernel",)},
-                 "lpc_env": ("fdlp::durbin4_kernel", "fdlp::durbin8_kernel", "fdlp::lpc_env_lattice_kernel", "fdlp::cep_kernel",
-                             "fdlp::env_gemm_kernel", "fdlp::ola_fixup"),
+                 "lpc_env": ("fdlp::durbin4_kernel", "fdlp::durbin8_kernel", "fdlp::lpc_env_lattice_kernel",
+                             "fdlp::lpc_env_kernel"),
                  "ola_log": ("fdlp::ola_log",)}
 
 
@@ -363,18 +363,11 @@ RANK_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR
             "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID")
 
 
-def child_inflight(args):
-    """batches in flight of each --xfer-procs child: --xfer-child-inflight, or the rank's share of --inflight"""
-    return args.xfer_child_inflight or max(1, args.inflight // max(1, args.xfer_procs))
-
-
-def xfer_child_spec(args, world, rank, local, argv=None, environ=None, j=0, procs=1):
+def xfer_child_spec(args, world, rank, local, argv=None, environ=None):
     """argv and environment of the PCIe-pass child of one rank (started before the rank touches the GPU):
     a single-process bench.py --xfer-only over the rank's own shard (--xfer-shard rank/world), on the rank's
     GPU only (HIP_VISIBLE_DEVICES narrowed to it), with GPU_MAX_HW_QUEUES = --xfer-hw-queues (read once per
-    process, so the rank's own timed steps keep the default), and no rendezvous variables.
-    procs > 1: child j of the rank's `procs` takes shard rank * procs + j of world * procs, 1/procs of the
-    batches in flight, and meets its siblings at a start barrier (--xfer-barrier)."""
+    process, so the rank's own timed steps keep the default), and no rendezvous variables."""
     argv = list(sys.argv[1:] if argv is None else argv)
     environ = os.environ if environ is None else environ
     out, skip = [], False
@@ -390,10 +383,7 @@ def xfer_child_spec(args, world, rank, local, argv=None, environ=None, j=0, proc
         if a.startswith("--gpus=") or a.startswith("--xfer-shard="):
             continue
         out.append(a)
-    out += ["--xfer-only", "--no-cpu-baseline", "--gpus", "1",
-            "--xfer-shard", "%d/%d" % (rank * procs + j, world * procs)]
-    if procs > 1:
-        out += ["--inflight", str(child_inflight(args)), "--xfer-variants", "", "--xfer-barrier"]
+    out += ["--xfer-only", "--no-cpu-baseline", "--gpus", "1", "--xfer-shard", "%d/%d" % (rank, world)]
     env = {k: v for k, v in environ.items() if k not in RANK_ENV}
     env["GPU_MAX_HW_QUEUES"] = str(args.xfer_hw_queues)
     if world > 1:
@@ -426,88 +416,15 @@ def combine_xfer_children(got):
     x["audio_h"] = sum(g["audio_h"] for g in got)
     x["elapsed_s"] = wall
     x["per_rank_value"] = [g["value"] for g in got]
-    for k in ("float32_d2h", "mapped_codes", "t_go"):
-        x.pop(k, None)
+    x.pop("t_go", None)
     x["note"] = (x.get("note", "") + "; one child process per rank on its own GPU, started before the rank "
                  "touches it, all at once: value = total audio / first start to last end")
-    return x
-
-
-def run_xfer_children(args, world=1, rank=0, local=0):
-    """--xfer-procs P > 1: P PCIe-pass children of this rank on its GPU at once (as the recipe runs several
-    JOBs per GPU), each over its shard with 1/P of the batches in flight.  Every child reports when its
-    warmup is done and waits; all are released together, and value = their total audio over the union of
-    their timed regions (first start to last end, absolute clocks).  None if any child fails."""
-    import tempfile
-    P = args.xfer_procs
-    procs, errs = [], []
-    for j in range(P):
-        argv, env = xfer_child_spec(args, world, rank, local, j=j, procs=P)
-        err = tempfile.TemporaryFile(mode="w+")
-        errs.append(err)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, text=True,
-                                      stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=err))
-    ok = True
-    for p in procs:  # each child's READY line (after its warmup)
-        while True:
-            line = p.stdout.readline()
-            if not line or line.strip() == "XFER_READY":
-                ok = ok and bool(line)
-                break
-    got = []
-    for p in procs:
-        try:
-            if ok:
-                p.stdin.write("go\n")
-            p.stdin.close()
-        except OSError:
-            ok = False
-    for p, err in zip(procs, errs):
-        out = p.stdout.read()  # stdin is closed and stderr goes to a file: one pipe, no deadlock
-        try:
-            p.wait(timeout=900)
-        except subprocess.TimeoutExpired:
-            p.kill()
-            p.wait()
-            ok = False
-        lines = [l for l in (out or "").strip().splitlines() if l.startswith("{")]
-        if p.returncode != 0 or not lines:
-            err.seek(0)
-            print("bench.py: PCIe-pass child failed (rc %s):\n%s" % (p.returncode, err.read()[-2000:]), file=sys.stderr)
-            ok = False
-        else:
-            got.append(json.loads(lines[-1])["with_transfers"])
-        err.close()
-    if not ok or len(got) != P:
-        return None
-    t0 = min(g["t_go"] for g in got)
-    t1 = max(g["t_go"] + g["elapsed_s"] for g in got)
-    x = dict(got[0])
-    x["audio_h"] = sum(g["audio_h"] for g in got)
-    x["elapsed_s"] = t1 - t0
-    x["value"] = x["audio_h"] / x["elapsed_s"]
-    x["ms_per_step"] = x["elapsed_s"] / args.steps * 1e3
-    x["h2d_bytes_per_step"] = sum(g["h2d_bytes_per_step"] for g in got)
-    x["d2h_bytes_per_step"] = sum(g["d2h_bytes_per_step"] for g in got)
-    x["codes_flagged_batches"] = sum(g["codes_flagged_batches"] for g in got)
-    x["codes_widen_bit_identical"] = all(g["codes_widen_bit_identical"] for g in got)
-    x["per_process_value"] = [g["value"] for g in got]
-    x["start_spread_s"] = max(g["t_go"] for g in got) - t0
-    x["processes_per_gpu"] = P
-    for k in ("float32_d2h", "mapped_codes", "t_go"):
-        x.pop(k, None)
-    x["note"] = ("%d processes on the GPU at once (the recipe runs several JOBs per GPU), each over its own "
-                 "utterances with %d batches in flight (the headline: %d), released together after their warmups: value "
-                 "= their total audio / first start to last end; per process: %s" %
-                 (P, child_inflight(args), args.inflight, got[0].get("note", "")))
     return x
 
 
 def run_xfer_child(args, world=1, rank=0, local=0):
     """bench.py --xfer-only in a child process (xfer_child_spec); its with_transfers block, or None (with
     the child's tail on stderr) when it fails."""
-    if args.xfer_procs > 1:
-        return run_xfer_children(args, world, rank, local)
     argv, env = xfer_child_spec(args, world, rank, local)
     try:
         p = subprocess.run([sys.executable, os.path.abspath(__file__)] + argv, env=env, capture_output=True,
@@ -555,30 +472,31 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
     The features leave the device as the compact ark codes (ABI 7, include/fdlp.h out_q_dev): int16
     k = nearbyint(v 10^3) per value, the ark's float32 (float)(k / 10^3) restored bit for bit on the host by
     fdlp_q_widen (the flag word of the batch, copied back with the codes, says whether every value had a
-    code; otherwise the batch's float32 rows, also written in HBM, are the ones to fetch).  Variants, same
-    steps: `float32_d2h` copies the float32 rows instead (ABI 6 protocol, twice the D2H bytes);
-    `mapped_codes`: the OLA kernel stores the codes straight into pinned host memory (no D2H copy)."""
+    code; otherwise the batch's float32 rows, also written in HBM, are the ones to fetch).  The widening of
+    every step's codes to the ark's float32 runs inside the timed region on a host thread pool, overlapped
+    with the next steps' copies and kernels (the float32 values an ark writer needs); the pass ends when the
+    last step's codes are widened.  (Schedules measured at or below this one and removed in round 6: 3-4
+    buffer sets, one grouped copy stream, host issue threads, per-batch H2D streams, float32 D2H, mapped
+    codes, several processes per GPU)"""
     import torch
+    from concurrent.futures import ThreadPoolExecutor
     from speech_recognition_tools_amd import q_widen
     out = outs[0]
     rows, D = out.shape
     nq = rows * D
     pin_in = torch.from_numpy(pcm_host).pin_memory()
-    grouped = args.xfer_schedule == "grouped"
-    S = max(3 if grouped else 1, args.xfer_sets)     # device buffer sets per batch, used in turn
+    S = 2                                            # device buffer sets per batch, used in turn
     NB = S * B                                       # (batch, step mod S)
     pcm_d = [pcms[i // S] if i % S == 0 else torch.empty_like(pcms[0]) for i in range(NB)]
     out_d = [outs[i // S] if i % S == 0 else torch.empty_like(out) for i in range(NB)]
     # codes + the flag word in one buffer: [nq int16 codes | int32 flag], one D2H copy per batch
     q_d = [torch.empty(nq + 2, dtype=torch.int16, device=dev) for _ in range(NB)]
     q_h = [torch.empty(nq + 2, dtype=torch.int16).pin_memory() for _ in range(NB)]
-    out_h = [torch.empty(out.shape, dtype=out.dtype).pin_memory() for _ in range(NB)]
-    s_ins = [torch.cuda.Stream(dev) for _ in range(max(1, args.xfer_h2d_streams))]
-    s_in = s_ins[0]
+    f_h = [np.empty(nq, dtype=np.float32) for _ in range(NB)]  # the widened ark values
+    s_in = torch.cuda.Stream(dev)
     nd = args.xfer_d2h_streams or (2 if args.xfer_only else 1)
     s_outs = [torch.cuda.Stream(dev) for _ in range(nd)]
-    nc = args.xfer_compute_streams or B
-    comp = [torch.cuda.current_stream(dev)] if B == 1 else [streams[b % nc] for b in range(B)]
+    comp = [torch.cuda.current_stream(dev)] if B == 1 else [streams[b] for b in range(B)]
     ev_in = [torch.cuda.Event() for _ in range(NB)]
     ev_done = [torch.cuda.Event() for _ in range(NB)]
     ev_out = [torch.cuda.Event() for _ in range(NB)]
@@ -586,123 +504,77 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
         ev_done[i].record(comp[(i // S) % len(comp)])
         ev_out[i].record(comp[(i // S) % len(comp)])
     it = [0]
-    mode = ["codes"]
+    widen_pool = ThreadPoolExecutor(1)               # one widening job at a time, each on 16 threads
+    widen_jobs = [None] * NB
+    widen_s = [0.0]
 
-    def copy_in(i):
-        si = s_in if grouped else s_ins[(i // S) % len(s_ins)]
-        si.wait_event(ev_done[i])                    # pcm_d[i] no longer read by its previous compute
-        with torch.cuda.stream(si):
+    def widen(i):
+        ev_out[i].synchronize()                      # the codes of buffer set i are on the host
+        t0 = time.perf_counter()
+        q_widen(q_h[i][:nq], 3, threads=16, out=f_h[i])
+        widen_s[0] += time.perf_counter() - t0
+
+    def xbatch(b, i):
+        cs = comp[b % len(comp)]
+        if widen_jobs[i] is not None:                # q_h[i] is read by the previous widening of set i
+            widen_jobs[i].result()
+        s_in.wait_event(ev_done[i])                  # pcm_d[i] no longer read by its previous compute
+        with torch.cuda.stream(s_in):
             pcm_d[i].copy_(pin_in, non_blocking=True)
-            ev_in[i].record(si)
-
-    def copy_out(b, i):
-        so = s_in if grouped else s_outs[b % nd]
+            ev_in[i].record(s_in)
+        cs.wait_event(ev_in[i])
+        cs.wait_event(ev_out[i])                     # q_d[i] copied out by its previous D2H
+        with torch.cuda.stream(cs):
+            flag = q_d[i][nq:].view(torch.int32)
+            flag.zero_()
+            plans[b].compute(pcm_d[i], lens, rng.randbits2(nj), out=out_d[i], out_q=q_d[i][:nq].view(rows, D),
+                             q_flag=flag, **mix[b])
+            ev_done[i].record(cs)
+        so = s_outs[b % nd]
         so.wait_event(ev_done[i])
         with torch.cuda.stream(so):
-            if mode[0] == "float32":
-                out_h[i].copy_(out_d[i], non_blocking=True)
-            else:
-                q_h[i].copy_(q_d[i], non_blocking=True)
+            q_h[i].copy_(q_d[i], non_blocking=True)
             ev_out[i].record(so)
-
-    def xbatch(b, i, h2d=True, d2h=True, jit=None):
-        cs = comp[b % len(comp)]
-        jit = rng.randbits2(nj) if jit is None else jit
-        if h2d:
-            copy_in(i)
-        cs.wait_event(ev_in[i])
-        cs.wait_event(ev_out[i])                     # out_d[i] / q_d[i] copied out by its previous D2H
-        with torch.cuda.stream(cs):
-            if mode[0] == "float32":
-                plans[b].compute(pcm_d[i], lens, jit, out=out_d[i], **mix[b])
-            else:
-                qt = q_h[i] if mode[0] == "mapped" else q_d[i]
-                flag = qt[nq:].view(torch.int32)
-                flag.zero_()
-                plans[b].compute(pcm_d[i], lens, jit, out=out_d[i], out_q=qt[:nq].view(rows, D),
-                                 q_flag=flag, **mix[b])
-            ev_done[i].record(cs)
-        if mode[0] == "mapped":
-            ev_out[i].record(cs)
-            return
-        if d2h:
-            copy_out(b, i)
-
-    nth = max(1, min(args.xfer_threads, B))
-    pool = None
-    if nth > 1:  # host threads issuing the batches (b = t, t + nth, ...); the jitter is drawn here, in order
-        from concurrent.futures import ThreadPoolExecutor
-        pool = ThreadPoolExecutor(nth)
+        widen_jobs[i] = widen_pool.submit(widen, i)
 
     def xstep():
         par = it[0] % S
         it[0] += 1
-        if pool is not None and not grouped:
-            jits = [rng.randbits2(nj) for _ in range(B)]
-            run = lambda t: [xbatch(b, S * b + par, jit=jits[b]) for b in range(t, B, nth)]
-            for fu in [pool.submit(run, t) for t in range(nth)]:
-                fu.result()
-            return
-        if not grouped:
-            for b in range(B):
-                xbatch(b, S * b + par)
-            return
-        # grouped: one copy stream carries step k + 1's copy-ins, then step k's copy-outs, so an H2D never
-        # overlaps a D2H (together they slow the D2H to a fifth of its rate, profiles/r05a_xfer_codes_timeline.txt)
-        if it[0] == 1:
-            for b in range(B):
-                copy_in(S * b + par)
         for b in range(B):
-            copy_in(S * b + (par + 1) % S)
-        for b in range(B):
-            xbatch(b, S * b + par, h2d=False, d2h=False)
-        if mode[0] != "mapped":
-            for b in range(B):
-                copy_out(b, S * b + par)
+            xbatch(b, S * b + par)
+
+    def xsync():                                     # the wall ends when the last codes are widened
+        for j in widen_jobs:
+            if j is not None:
+                j.result()
+        sync()
 
     cpu_dev = torch.device("cpu")
     from speech_recognition_tools_amd.shard import timed_steps
     t_go = [time.time()]
 
-    def start_barrier():  # --xfer-barrier: the parent releases its PCIe-pass children together
-        if args.xfer_barrier:
-            print("XFER_READY", flush=True)
-            sys.stdin.readline()
-        t_go[0] = time.time()  # absolute start of the timed region (children combine on the union)
-    el_x = timed_steps(xstep, args.steps, args.warmup, sync, dd, cpu_dev, before_timed=start_barrier)
+    def mark_start():
+        widen_s[0] = 0.0
+        t_go[0] = time.time()  # absolute start of the timed region (the ranks' children combine on the union)
+    el_x = timed_steps(xstep, args.steps, args.warmup, xsync, dd, cpu_dev, before_timed=mark_start)
+    widen_pool.shutdown()
     flags = [int(q[nq:].view(torch.int32)[0]) for q in q_h]
-    # the codes of the last steps' batches widen to the float32 rows still in HBM (bit-identical)
+    # the last step's widened codes equal the float32 rows still in HBM (bit-identical)
     par = (it[0] - 1) % S
-    wid = q_widen(q_h[par][:nq], 3, threads=16).reshape(rows, D)
-    same = bool(np.array_equal(wid.view(np.uint32), out_d[par].cpu().numpy().view(np.uint32)))
-    t0 = time.perf_counter()
-    for i in range(B):                               # host cost of the widening, one step's codes
-        q_widen(q_h[i][:nq], 3, threads=16, out=out_h[i].numpy().reshape(-1))
-    widen_s = time.perf_counter() - t0
+    same = bool(np.array_equal(f_h[par].view(np.uint32), out_d[par].cpu().numpy().reshape(-1).view(np.uint32)))
     ah = world * args.steps * B * audio_s / 3600.0
-    el_v = {}
-    for v in ("float32", "mapped"):
-        if v in args.xfer_variants.split(","):
-            mode[0] = v
-            el_v[v] = timed_steps(xstep, args.steps, 1, sync, dd, cpu_dev)
-    variant = lambda v, d: dict(value=ah / el_v[v], ms_per_step=el_v[v] / args.steps * 1e3, **d) if v in el_v else None
     return {"value": ah / el_x, "ms_per_step": el_x / args.steps * 1e3, "audio_h": ah, "elapsed_s": el_x,
             "t_go": t_go[0],
             "h2d_bytes_per_step": int(B * pcm_host.nbytes), "d2h_bytes_per_step": int(B * (nq + 2) * 2),
             "d2h_encoding": "compact ark codes: int16 nearbyint(v * 1e3) + an int32 flag per batch (ABI 7)",
             "codes_flagged_batches": sum(1 for f in flags if f), "codes_widen_bit_identical": same,
-            "host_widen_ms_per_step": widen_s * 1e3,
-            "host_widen_note": "fdlp_q_widen of one step's codes to float32 on 16 host threads (after the timed "
-                               "region: the float32 values an ark writer needs, outside 8(d)'s H2D..D2H wall)",
-            "float32_d2h": variant("float32", {"d2h_bytes_per_step": int(B * out.numel() * 4),
-                                               "note": "the same steps copying the float32 rows back (ABI 6 "
-                                                       "protocol)"}),
-            "mapped_codes": variant("mapped", {"note": "the OLA kernel stores the codes straight into pinned host "
-                                                       "memory (fdlp_mapped_ptr) instead of a D2H copy"}),
-            "note": "every batch's PCM copied in from pinned host memory and its compact feature codes copied "
-                    "back every step (%d batch(es) in flight on %d compute stream(s), %d device buffer sets per "
-                    "batch used in turn, one H2D stream, %d D2H stream(s)); not the headline (inputs "
-                    "resident in HBM)" % (B, len(comp), S, nd)}
+            "host_widen_ms_per_step": widen_s[0] / args.steps * 1e3,
+            "host_widen_note": "fdlp_q_widen of every batch's codes to the ark's float32 on 16 host threads, inside "
+                               "the timed region (overlapped with the next steps' copies and kernels)",
+            "note": "every batch's PCM copied in from pinned host memory, its compact feature codes copied back "
+                    "and widened to float32 on the host, every step (%d batch(es) in flight on %d compute "
+                    "stream(s), %d device buffer sets per batch used in turn, one H2D stream, %d D2H stream(s))"
+                    % (B, len(comp), S, nd)}
 
 
 def parse_args(argv=None):
@@ -727,33 +599,10 @@ def parse_args(argv=None):
                     help="PCIe pass: every rank runs it in a child process (started before the rank touches the "
                          "GPU) with GPU_MAX_HW_QUEUES set to this (the compute, H2D and D2H streams then get hardware "
                          "queues of their own; 0: in-process, with the process default of 4)")
-    ap.add_argument("--xfer-variants", default="float32,mapped",
-                    help="PCIe pass: the variants timed after the compact-code pass (float32 D2H, mapped codes)")
     ap.add_argument("--xfer-only", action="store_true", help=argparse.SUPPRESS)  # the PCIe-pass child
     ap.add_argument("--xfer-shard", default=None, help=argparse.SUPPRESS)  # rank/world of the child's shard
-    ap.add_argument("--xfer-sets", type=int, default=2,
-                    help="PCIe pass: device buffer sets per batch in flight, used in turn (2: step s + 1's copy-in "
-                         "overlaps step s's kernels and step s - 1's copy-out)")
-    ap.add_argument("--xfer-schedule", default="streams", choices=["streams", "grouped"],
-                    help="PCIe pass: streams = copy-ins on one stream, copy-outs on --xfer-d2h-streams others; "
-                         "grouped = one copy stream, each step's next copy-ins then its copy-outs (3+ buffer sets)")
-    ap.add_argument("--xfer-procs", type=int, default=1,
-                    help="PCIe pass: child processes on each GPU at once, each with 1/P of the batches in flight "
-                         "over its own utterances (the recipe runs several JOBs per GPU)")
-    ap.add_argument("--xfer-child-inflight", type=int, default=0,
-                    help="PCIe pass with --xfer-procs: batches in flight per process (0: --inflight / P)")
-    ap.add_argument("--xfer-barrier", action="store_true", help=argparse.SUPPRESS)  # child of --xfer-procs > 1
-    ap.add_argument("--xfer-h2d-streams", type=int, default=1,
-                    help="PCIe pass: host-to-device copy streams (batch b on stream b mod n)")
-    ap.add_argument("--xfer-threads", type=int, default=1,
-                    help="PCIe pass: host threads issuing the batches' copies and kernels (batch b on thread b mod T)")
-    ap.add_argument("--xfer-compute-streams", type=int, default=0,
-                    help="PCIe pass: compute streams for the batches in flight (0: one per batch)")
-    ap.add_argument("--pipeline", type=int, default=None, help="sub-batches over two streams (plan default 1)")
     ap.add_argument("--dct-path", default="auto", choices=["auto", "four_step"],
                     help="DCT stage: auto (one dct_frame_kernel per frame at N = 24000) or the four-step pair")
-    ap.add_argument("--ola-path", default="auto", choices=["auto", "separate", "fused"],
-                    help="OLA + log stage (A/B): auto = separate (ola_log_tiled_kernel); fused = inside the LPC kernel")
     ap.add_argument("--lpc-path", default="auto", choices=["auto", "lattice8", "lds"],
                     help="Durbin kernel (A/B): auto = durbin4_kernel for the recipes' p = 150")
     ap.add_argument("--inflight", type=int, default=4,
@@ -872,8 +721,6 @@ def main():
     audio_s = sum(lens) / 16000.0
 
     plan = FdlpPlan(cfg, device=dev.index, max_frames=frames)
-    if args.pipeline is not None:
-        plan.set_pipeline(args.pipeline)
     _, lo, hi = probe.fbank()
     support = (hi - lo).astype(np.int64)
 
@@ -893,7 +740,6 @@ def main():
     for pl in plans:
         pl.set_dct_path(args.dct_path)
         pl.set_lpc_path(args.lpc_path)
-        pl.set_ola_path(args.ola_path)
     shifts = [7919 * b for b in range(B)]
     pcms = [pcm] + [torch.roll(pcm, shifts[b]) for b in range(1, B)]
     outs = [out] + [torch.empty_like(out) for _ in range(B - 1)]
@@ -930,9 +776,10 @@ def main():
     # 2) one batch per step with per-stage HIP events on the stream the kernels run on (roofline: the
     #    kernels alone, not overlapped with another batch's)
     if not args.xfer_only:
-        plan.set_profiling(True)
+        plan.set_profiling(True, kernels=True)
         elapsed_prof = timed_steps(step, args.steps, 0, sync, dd, cpu_dev)
         stages, ncalls = plan.stage_times()
+        kern = plan.kernel_times()
         plan.set_profiling(False)
 
     # 3) PCIe-inclusive: PCM copied in from pinned host memory and float32 features back to pinned host
@@ -965,6 +812,14 @@ def main():
     stage_ms = {"dct": sms["frames_dft1"] + sms["dft2_dct"], "autocorr": sms["autocorr"],
                 "lpc_env": sms["lpc_env"], "ola_log": sms["ola_log"]}
     dom = max(stage_ms, key=stage_ms.get)
+    # per-kernel HIP events of the same profiled pass: ms per launch of every kernel, and the dominant stage's
+    # kernels summed (the roofline's time: the kernels themselves, comparable kernel by kernel with a rocprofv3
+    # trace of the same command)
+    kernel_ms = {k: ms / max(n, 1) for k, (ms, n) in kern.items()}
+    kernel_launches_per_batch = {k: n / max(ncalls, 1) for k, (ms, n) in kern.items()}
+    dom_prefixes = stage_kernel_prefixes(dom, plan.autocorr_path)
+    dom_kernels = {k: v * kernel_launches_per_batch[k] for k, v in kernel_ms.items()
+                   if any(k.startswith(pre) for pre in dom_prefixes)}
     items = frames * plan.B
     Me = min(cfg.coeff_num, 2 * plan.kk)
     stage_flops = {"dct": dct_flops(plan.N) * frames, "autocorr": autocorr_flops(plan, support) * frames,
@@ -973,7 +828,7 @@ def main():
     pmc_file = _latest_pmc(args.config if args.workload != "librispeech" else "librispeech") or PMC_FILE
     path = plan.autocorr_path
     traffic, bound = stage_pmc(stage_kernel_prefixes(dom, path), pmc_file)
-    dom_ms = stage_ms[dom]
+    dom_ms = sum(dom_kernels.values()) if dom_kernels else stage_ms[dom]
     achieved = stage_flops[dom] / (dom_ms * 1e-3) / 1e12
     ac_can, whole_can = canonical_flops(plan.N, plan.B, cfg.order, cfg.coeff_num, plan.kk, 2 * plan.kk)
     # algorithmic HBM bytes (north_star / SURVEY 8(d)): int16 PCM in + float32 features out
@@ -1026,13 +881,16 @@ def main():
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_unit": "bytes/launch (rocprofv3 PMC, %s)" % os.path.relpath(pmc_file or "none", ROOT),
                      "avg_launch_ms": dom_ms, "algorithmic_flops_per_launch": stage_flops[dom],
-                     "timing": ("avg_launch_ms = HIP events recorded around the stage's kernels on the stream they "
-                                "run on (fdlp_stage_times), one batch in flight, mean over the %d profiled steps of "
-                                "this run; achieved = algorithmic_flops_per_launch / avg_launch_ms.  The events "
-                                "include the launch gaps between the stage's kernels, so a kernel-trace sum of "
-                                "the kernels below is at most this (scripts/round_evidence.sh writes both side "
-                                "by side: <tag>_frac_check.json)" % args.steps),
+                     "timing": ("avg_launch_ms = the sum of the stage's kernels (kernel_ms_per_batch), each timed by "
+                                "the HIP events recorded right before and after it on the stream it runs on "
+                                "(fdlp_set_profiling(plan, 2) / fdlp_kernel_times), one batch in flight, mean over "
+                                "the %d profiled steps of this run; achieved = algorithmic_flops_per_launch / "
+                                "avg_launch_ms.  scripts/round_evidence.sh compares these kernel by kernel with a "
+                                "rocprofv3 trace of the same command (<tag>_frac_check.json); stage_span_ms is the "
+                                "per-stage event span (launch gaps included)" % args.steps),
                      "stage_kernels": list(stage_kernel_prefixes(dom, path)),
+                     "kernel_ms_per_batch": dom_kernels,
+                     "stage_span_ms": stage_ms[dom],
                      "stage_fracs": {k: stage_flops[k] / (stage_ms[k] * 1e-3) / 1e12 / FP64_PEAK_TFLOPS
                                      for k in stage_ms if stage_ms[k] > 0},
                      "canonical_frac": ac_can * frames / (sms["autocorr"] * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
@@ -1044,6 +902,7 @@ def main():
                                        (ac_can / 1e6, whole_can / 1e6)},
         "hbm": hbm,
         "stage_ms_per_step": sms,
+        "kernel_ms_per_launch": kernel_ms,
         "ms_per_batch_profiled": elapsed_prof / args.steps * 1e3,
         "one_batch_in_flight": {"value": world * args.steps * audio_s / 3600.0 / elapsed_one,
                                 "ms_per_step": elapsed_one / args.steps * 1e3,

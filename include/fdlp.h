@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define FDLP_ABI_VERSION 8
+#define FDLP_ABI_VERSION 9
 
 enum {
   FDLP_OK = 0,
@@ -199,21 +199,6 @@ int fdlp_set_lpc_path(fdlp_plan* plan, int32_t path);
 #define FDLP_DCT_FRAME 2
 int fdlp_set_dct_path(fdlp_plan* plan, int32_t path);
 int fdlp_dct_path(const fdlp_plan* plan);
-/* OLA + log stage (ABI 7).  FDLP_OLA_AUTO (plan default) = FDLP_OLA_SEPARATE: ola_log_tiled_kernel after the
- * LPC kernel (computeFDLPSpectrogram.py:207-229).  FDLP_OLA_FUSED: for the spectrogram with the lattice LPC
- * kernels the overlap-add, floor and log run inside the LPC kernel -- each wave runs consecutive frames of one
- * utterance for 4 bands and adds each frame's envelope into the output rows it owns with the previous
- * frame's tail, in the reference's frame order (bit-identical to the separate kernel) -- so the envelopes
- * never go to HBM; it falls back to the separate kernel where a row is covered by more than two frames, with
- * sub-batch pipelining and for the LDS Durbin.  Measured slower on MI355X than the separate kernel (DESIGN.md
- * §4 item 5), so not the default.  fdlp_ola_path returns the stage the last fdlp_compute ran
- * (FDLP_OLA_FUSED or FDLP_OLA_SEPARATE; 0 before any / modulation spectrum).  After a fused compute,
- * fdlp_debug_fetch returns envelopes only if fdlp_set_debug(plan, 1) was set. */
-#define FDLP_OLA_AUTO 0
-#define FDLP_OLA_SEPARATE 1
-#define FDLP_OLA_FUSED 2
-int fdlp_set_ola_path(fdlp_plan* plan, int32_t path);
-int fdlp_ola_path(const fdlp_plan* plan);
 /* Lower-skirt / flat-top / upper-skirt split of every band, [0,m1) [m1,m2) [m2,N), used by the
  * STRUCTURED path; FDLP_E_INVALID when the filterbank does not have it. */
 int fdlp_plan_regions(const fdlp_plan* plan, int32_t* m1, int32_t* m2);
@@ -229,13 +214,13 @@ int fdlp_plan_flat_events(const fdlp_plan* plan, int32_t* chains, int32_t* parts
 int fdlp_set_pipeline(fdlp_plan* plan, int32_t n_sub);
 /* Reads back the intermediates of the most recent fdlp_compute (parity/debug; synchronous):
  * any pointer may be NULL.  Layouts: dct [F,N]; r [F,B,nlags]; a [F,B,order+1]; gg [F,B];
- * cep [F,B,coeff_num]; env [F,B,kk] (fused OLA: only after fdlp_set_debug(plan, 1), ABI 7). */
+ * cep [F,B,coeff_num]; env [F,B,kk] (spectrogram plans).  ABI 9 removed the fused OLA stage
+ * (fdlp_set_ola_path / fdlp_ola_path, measured slower than the separate OLA kernel). */
 int fdlp_debug_fetch(fdlp_plan* plan, int32_t n_frames, double* dct, double* r, double* a,
                      double* gg, double* cep, double* env);
 /* Same for the frames [first_frame, first_frame + n_frames) of the most recent batch (ABI 3).
  * a and cep need fdlp_set_debug(plan, 1) before that compute (their workspaces are allocated by it;
- * FDLP_E_INVALID otherwise), and so does env when that compute fused the OLA (ABI 7); dct, r and gg are
- * always available. */
+ * FDLP_E_INVALID otherwise); dct, r, gg and (spectrogram plans) env are always available. */
 int fdlp_debug_fetch_range(fdlp_plan* plan, int32_t first_frame, int32_t n_frames, double* dct, double* r,
                            double* a, double* gg, double* cep, double* env);
 
@@ -247,6 +232,13 @@ int fdlp_debug_fetch_range(fdlp_plan* plan, int32_t first_frame, int32_t n_frame
 #define FDLP_NUM_STAGES 5
 int fdlp_set_profiling(fdlp_plan* plan, int32_t enable);
 int fdlp_stage_times(fdlp_plan* plan, double* ms_sum /* [FDLP_NUM_STAGES] */, int32_t* n_calls);
+/* Per-kernel device time (ABI 9): with fdlp_set_profiling(plan, 2) every kernel launch of an fdlp_compute
+ * (one sub-batch) is followed by a HIP event on the stream it runs on, and the time between consecutive
+ * events -- one kernel each, the stage's launch gaps included -- is summed per kernel id.  fdlp_kernel_name
+ * gives the id's kernel (the rocprofv3 name prefix, e.g. "fdlp::ac_band_kernel"); launches counts them. */
+#define FDLP_NUM_KERNELS 16
+int fdlp_kernel_times(fdlp_plan* plan, double* ms_sum /* [FDLP_NUM_KERNELS] */, int64_t* launches);
+const char* fdlp_kernel_name(int32_t id);
 /* Seconds fdlp_plan_create spent in: [0] host tables (filterbank, structured-autocorrelation tables,
  * weights), [1] device open + table uploads, [2] LPC kernel launch setup, [3] workspace allocation,
  * [4] total (a cold JOB's fixed cost, benchmarks/cold_start_probe.py; ABI 4). */

@@ -1,4 +1,4 @@
-# A/B of bench variants on one box, alternating: AB_ARGS="--ola-path auto|--ola-path separate" TAG=x bash scripts/gpu_ab.sh
+# A/B of bench variants on one box, alternating: AB_ARGS="--lpc-path auto|--lpc-path lattice8" TAG=x bash scripts/gpu_ab.sh
 set -u
 cd "${GRAFT_REPO_ROOT}"
 export TMPDIR=/tmp

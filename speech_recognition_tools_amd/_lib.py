@@ -33,13 +33,14 @@ FDLP_PCM_F64 = 1
 FDLP_PRE_NONE = 0
 FDLP_PRE_DIFF = 1
 FDLP_NUM_STAGES = 5
+FDLP_NUM_KERNELS = 16
 FDLP_MODE_SPECTROGRAM = 0
 FDLP_MODE_MODSPEC = 1
 FDLP_MODE_MODSPEC_COMPLEX = 2
 FDLP_WIN_HAMMING = 0
 FDLP_WIN_HANNING = 1
 FDLP_WIN_RECT = 2
-ABI_VERSION = 8
+ABI_VERSION = 9
 FDLP_FN_LOG, FDLP_FN_EXP = 0, 1  # fdlp_device_fn
 STAGE_NAMES = ("frames_dft1", "dft2_dct", "autocorr", "lpc_env", "ola_log")
 
@@ -140,9 +141,9 @@ SIGNATURES = {
     "fdlp_set_dct_path": (c_i32, [c_p, c_i32]),
     "fdlp_dct_path": (c_i32, [c_p]),
     "fdlp_set_pipeline": (c_i32, [c_p, c_i32]),
-    "fdlp_set_ola_path": (c_i32, [c_p, c_i32]),
-    "fdlp_ola_path": (c_i32, [c_p]),
     "fdlp_stage_times": (c_i32, [c_p, P_dbl, P_i32]),
+    "fdlp_kernel_times": (c_i32, [c_p, P_dbl, P_i64]),
+    "fdlp_kernel_name": (ctypes.c_char_p, [c_i32]),
     "fdlp_plan_setup_times": (c_i32, [c_p, P_dbl]),
     "fdlp_dct_rows": (c_i32, [c_p, c_p, c_i32, c_p, c_p]),
     "fdlp_lpc_rows": (c_i32, [c_p, c_p, c_i32, c_p, c_p, c_p, c_p]),

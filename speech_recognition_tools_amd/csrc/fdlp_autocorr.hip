@@ -915,6 +915,7 @@ template <int NT>
 static hipError_t launch_ac_nt(const DevConsts& c, const double* dct, const double* dense, int items,
                                double* r, hipStream_t s) {
   hipLaunchKernelGGL((autocorr_kernel<NT>), dim3(items), dim3(64), 0, s, c, dct, dense, r);
+  (void)kmark(kKAutocorr, s);
   return hipGetLastError();
 }
 
@@ -961,8 +962,10 @@ static hipError_t launch_vsweep_ac(const DevConsts& c, const double* dct, int nf
   const int ngroups = (nframes + 3) / 4;
   hipLaunchKernelGGL((ac_vsweep_kernel<A, 0>), dim3(xcd_grid(2 * ngroups)), dim3(64), 0, s, c, dct, r, rup, rflat,
                      rpart, c.sk_snap, c.fl_ev, nframes, ngroups);
+  (void)kmark(kKVsweepSkirt, s);
   hipLaunchKernelGGL((ac_vsweep_kernel<A, C>), dim3(xcd_grid(c.fl_H * ngroups)), dim3(64), 0, s, c, dct, r, rup,
                      rflat, rpart, c.sk_snap, c.fl_ev, nframes, ngroups);
+  (void)kmark(kKVsweepFlat, s);
   return hipGetLastError();
 }
 template <int A>
@@ -993,15 +996,21 @@ static hipError_t launch_struct_nt(const DevConsts& c, const double* dct, int nf
     const hipError_t e = launch_vsweep(c, dct, nframes, r, rup, rflat, rpart, s);
     if (e != hipSuccess) return e;
     const bool wrap = rwrap && c.sk_wrap && c.nlags <= kMaxWrapLags;
-    if (wrap) hipLaunchKernelGGL(ac_wrap_kernel, dim3(nframes), dim3(64), 0, s, c, dct, rwrap, nframes);
+    if (wrap) {
+      hipLaunchKernelGGL(ac_wrap_kernel, dim3(nframes), dim3(64), 0, s, c, dct, rwrap, nframes);
+      (void)kmark(kKAcWrap, s);
+    }
     hipLaunchKernelGGL((ac_band_kernel<NT, true>), dim3(xcd_grid(nframes * c.B)), dim3(64), 0, s, c, dct, r, rup,
                        rflat, rpart, wrap ? rwrap : nullptr, nframes * c.B);
+    (void)kmark(kKAcBand, s);
     return hipGetLastError();
   }
   const size_t tab = sizeof(SkSnap) * (size_t)c.B;
   hipLaunchKernelGGL((ac_sweep_kernel<NT, 32>), dim3(xcd_grid(2 * nframes)), dim3(64), tab, s, c, dct, r, rup, 2 * nframes);
+  (void)kmark(kKAcSweep, s);
   hipLaunchKernelGGL((ac_band_kernel<NT, false>), dim3(xcd_grid(nframes * c.B)), dim3(64), 0, s, c, dct, r, rup,
                      nullptr, nullptr, nullptr, nframes * c.B);
+  (void)kmark(kKAcBand, s);
   return hipGetLastError();
 }
 

@@ -872,6 +872,7 @@ hipError_t launch_dct_frame(const DevConsts& c, const void* pcm, int pcm_kind, c
   const int grid = (nframes + kDctFramesPerBlock - 1) / kDctFramesPerBlock;
   hipLaunchKernelGGL(dct_frame_kernel, dim3(grid), dim3(dct1::kThreads), 0, s, c, pcm, pcm_kind, noise, frames,
                      dense_rows, nframes, sc2, dct);
+  (void)kmark(kKDctFrame, s);
   return hipGetLastError();
 }
 
@@ -888,16 +889,19 @@ hipError_t launch_frames_dft1(const DevConsts& c, const DftPlan& d1, int N2, con
   if (c.real_fft && d1.n == 100 && N2 == 120 && !dense_rows) {  // recipes: N = 24000
     hipLaunchKernelGGL((frames_dft1_c_kernel<100, 120, kDftCols>), dim3(xcd_grid(grid.x * nframes)), dim3(256), 0, s, c,
                        pcm, pcm_kind, noise, frames, om1, z, nframes);
+    (void)kmark(kKFramesDft1, s);
     return hipGetLastError();
   }
   if (c.real_fft) {
     if (lds > 65536) (void)hipFuncSetAttribute((const void*)frames_dft1_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(frames_dft1_kernel<true>, grid, dim3(256), lds, s, c, d1, N2, pcm, pcm_kind, noise,
                        frames, dense_rows, om1, z);
+    (void)kmark(kKFramesDft1, s);
   } else {
     if (lds > 65536) (void)hipFuncSetAttribute((const void*)frames_dft1_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(frames_dft1_kernel<false>, grid, dim3(256), lds, s, c, d1, N2, pcm, pcm_kind, noise,
                        frames, dense_rows, om1, z);
+    (void)kmark(kKFramesDft1, s);
   }
   return hipGetLastError();
 }
@@ -912,16 +916,19 @@ hipError_t launch_dft2_dct(const DevConsts& c, const DftPlan& d2, int N1, const 
     const dim3 g1(xcd_grid(grid.x * nframes));
     const double sc2 = 2.0 / div;
     hipLaunchKernelGGL((dft2_dct_c_kernel<100, 120, kDftCols, true>), g1, dim3(256), 0, s, c, z, om2, sc2, dct, nframes);
+    (void)kmark(kKDft2Dct, s);
     return hipGetLastError();
   }
   if (c.real_fft) {
     dim3 grid((N1 / 2 + 1 + kDftCols / 2 - 1) / (kDftCols / 2), nframes);  // row pairs (k1, N1-k1)
     if (lds > 65536) (void)hipFuncSetAttribute((const void*)dft2_dct_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(dft2_dct_kernel<true>, grid, dim3(256), lds, s, c, d2, N1, z, om2, div, dct);
+    (void)kmark(kKDft2Dct, s);
   } else {
     dim3 grid((N1 + kDftCols - 1) / kDftCols, nframes);
     if (lds > 65536) (void)hipFuncSetAttribute((const void*)dft2_dct_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(dft2_dct_kernel<false>, grid, dim3(256), lds, s, c, d2, N1, z, om2, div, dct);
+    (void)kmark(kKDft2Dct, s);
   }
   return hipGetLastError();
 }

@@ -298,7 +298,7 @@ __device__ __forceinline__ int16_t q_code(double k, bool& bad) {
 
 // One feature of the OLA output (computeFDLPSpectrogram.py:227-229): log(clip(acc, 1e-14)) keeping NaN,
 // stored as fp64 (debug), float32 ('%.<d>f'-rounded when decimals >= 0) and / or compact code; the OLA
-// kernel, the fused OLA of the lattice kernel and the boundary fixup all store through this.
+// kernel stores through this.
 // np.log of the OLA sums (computeFDLPSpectrogram.py:227) in ~35 VALU operations instead of the ~65 of
 // ocml's log: x = 2^e m with m in [sqrt(1/2), sqrt(2)) (so e = 0 around 1: no ln 2 cancellation),
 // i = round(128 m), c = i / 128, u = m - c exactly (Sterbenz), r = u RN(1/c) (|r| < 2^-7.5),

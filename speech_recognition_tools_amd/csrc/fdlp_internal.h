@@ -38,22 +38,6 @@ struct UttDesc {
   int32_t pad;
 };
 
-// Fused OLA + log (lpc_env_lattice_kernel<..., OLA = true>): one chunk = consecutive frames of one utterance
-// that a wave runs in order for one band quad (4 bands), carrying each frame's tail (the rows the next frame
-// also covers) to the next.  Long utterances are cut into chunks between two middle frames (full kk, src 0);
-// such a boundary's overlap rows are finished by ola_fixup_kernel from the two partial sums.
-struct OlaChunk {
-  int32_t frame0;   // first analysis frame (batch index)
-  int32_t nf;       // frames
-  int32_t bin;      // boundary whose second half this chunk's first frame writes (fa), -1: none
-  int32_t bout;     // boundary whose first half this chunk's last frame writes (fb), -1: none
-};
-struct OlaBound {
-  int64_t row0;     // absolute output row of the second frame's dst
-  int32_t len;      // overlap rows (first frame's dst + kk - second frame's dst)
-  int32_t pad;
-};
-
 // One snapshot of a skirt sweep: after the positions >= S are consumed, band `band` receives
 // K times the truncated autocorrelation (structured autocorrelation, fdlp_autocorr.hip 3s).
 struct SkSnap {
@@ -116,6 +100,20 @@ struct DevConsts {
   const double2* dct1_tw = nullptr;  // dct_frame_kernel tables (N = 24000 only; see dct_frame_tables)
 };
 
+// Per-kernel HIP-event marks (fdlp_set_profiling(plan, 2), fdlp_kernel_times): while a profiled fdlp_compute
+// issues its kernels, each launch site calls kmark(id, stream) after its launch, which records an event on
+// that stream when marks are being collected on this thread (g_kmarks), and does nothing otherwise.
+enum KernelId {
+  kKDctFrame = 0, kKFramesDft1, kKDft2Dct, kKVsweepSkirt, kKVsweepFlat, kKAcWrap, kKAcBand, kKAcSweep,
+  kKAutocorr, kKDurbin4, kKDurbin8, kKLattice, kKLpcLds, kKOlaLog, kKOther, kKCount
+};
+struct KMark {
+  int id;
+  hipEvent_t ev;
+};
+extern thread_local std::vector<KMark>* g_kmarks;
+hipError_t kmark(int id, hipStream_t s);
+
 }  // namespace fdlp
 
 // Launch wrappers implemented in fdlp_{dct,autocorr,lpc,misc}.hip (host-callable).
@@ -159,29 +157,9 @@ hipError_t launch_cepstrum(int p, int M, const double* a, const double* gg, int 
                            double* cep, hipStream_t s);
 // a_ws / gg_ws: [items, c.lpc_astride] / [items] workspace of the split Durbin (durbin8_kernel,
 // c.lpc_split); a_out / gg_out (debug, [items, p+1] / [items]) get copies
-// Output side of the fused OLA (computeFDLPSpectrogram.py:207-229 inside the lattice kernel); null: the
-// envelopes go to `env` and ola_log_tiled_kernel runs after
-struct OlaFused {
-  const FrameDesc* frames;
-  const UttDesc* utts;
-  const OlaChunk* chunks;   // sorted by nf, longest first
-  const OlaBound* bounds;
-  int nchunks, nbounds;
-  int* counter;             // [8] per-XCD work counters, zeroed on the stream before the launch
-  double* ring;             // [grid, 2, 4, kk] per-wave tails
-  double* fa;               // [nbounds, B, kk] second frame's overlap values
-  double* fb;               // [nbounds, B, kk] first frame's overlap values
-  float* out;
-  double* out64;
-  int16_t* outq;
-  uint32_t* qflag;
-  int decimals;
-};
 hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int items, double* env,
                           double* a_out, double* gg_out, double* cep_out, double* a_ws, double* gg_ws,
-                          hipStream_t s, const OlaFused* ola = nullptr);
-// true when launch_lpc_env can fuse the OLA for this plan (the lattice kernels run)
-bool lpc_env_can_fuse(const DevConsts& c);
+                          hipStream_t s);
 int lpc_env_region(int p, int M);
 // Per-plan launch setup of launch_lpc_env for the current device: sets the kernel's large-LDS
 // attribute and stores the resident block count in c.lpc_blocks.

@@ -725,7 +725,8 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
   }
   stats.n_lines = (int64_t)lines.size();
 
-  Reader reader(lines, std::max(1, o->io_threads), 512);  // reading starts while the plan is built
+  constexpr int kReadDepth = 512;  // entries the readers run ahead of the consumer
+  Reader reader(lines, std::max(1, o->io_threads), kReadDepth);  // reading starts while the plan is built
 
   fdlp_config c = *cfg;
   c.max_frames = std::max(1, o->batch_frames);
@@ -754,8 +755,9 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     std::vector<size_t> want_smp(slots.size(), pin_smp), want_rows(slots.size(), pin_rows);
     std::vector<int64_t> lens;
     // (a job that has read a full batch of samples already gets full-size slots: no wait beyond that; a
-    // scp of more than kSizeLines entries is taken as large without waiting, so its pinning starts at once)
-    constexpr size_t kSizeLines = 4096;
+    // scp of more than the readers' depth is taken as large without waiting, so its pinning starts at once:
+    // the readers park at that depth until the consumer, which waits for `sized`, takes entries)
+    constexpr size_t kSizeLines = kReadDepth;
     if (cold && reader.size() <= kSizeLines && reader.wait_lengths((int64_t)pin_smp, 10, &lens)) {
       std::vector<size_t> ns, nr;
       slot_needs(lens, c, slots.size(), &ns, &nr);
@@ -902,7 +904,9 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     }
     trace.add("closed");
     bool parked = false;
-    if (o->keep_warm && code == FDLP_OK && s && s_in && s_out) {  // park for the next call
+    // park for the next call -- only a plan of the key's batch size: a long utterance that rebuilt the plan
+    // (c.max_frames = F) would otherwise leave its larger plan under the original key
+    if (o->keep_warm && code == FDLP_OK && s && s_in && s_out && c.max_frames == key.max_frames) {
       bool all_pinned = true;
       for (auto& sl : slots) all_pinned = all_pinned && sl.pinned && !sl.busy;
       if (all_pinned) {

@@ -160,11 +160,6 @@ struct LpcEnvArgs {
   const double* a_ext;    // DM = 2: a [items, a_stride] and gg [items] from durbin8_kernel
   const double* gg_ext;
   int a_stride;
-  // fused OLA + log (lpc_env_lattice_kernel<..., OLA = true>; env is then written only when non-null, for
-  // fdlp_debug_fetch): the chunk table, the bands, the outputs (OlaFused)
-  int B, nbq, nunits, decimals;
-  double scale10;
-  OlaFused ola;
 };
 
 // Durbin recursion with a[] resident in LDS (la[0..p], zero beyond) and r in LDS (lr): lane l of
@@ -964,14 +959,7 @@ __device__ __forceinline__ double inv_count(int n) {
 // LDS allows 2.5 per SIMD anyway
 template <int CB>
 constexpr int lat_waves() { return CB < 0 ? 2 : 4; }
-// OLA (computeFDLPSpectrogram.py:207-229 fused, OlaFused): the waves take chunks of consecutive frames of
-// one utterance x band quad from a work counter (longest chunks first) and run the chunk's frames in order,
-// so each frame's envelope goes straight to the output rows it owns, (0 + tail of the previous frame) + own
-// sample in the reference's frame order, then log / clip / rounding (ola_store_feature); the rows the next
-// frame also covers stay in a per-wave ring (L2) as its tail.  Chunk edges inside an utterance leave their
-// overlap rows' two halves in fa / fb for ola_fixup_kernel.  Needs every row covered by at most two frames
-// (checked on the host).
-template <int SL, int CB = 0, int DM = kDmContig, bool OLA = false>
+template <int SL, int CB = 0, int DM = kDmContig>
 __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(LpcEnvArgs A_) {
   extern __shared__ double sh[];
   const LpcEnvArgs& A = A_;
@@ -1002,47 +990,14 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
       }
     }
   };
-  // ---- group sequence: first item of each group of 4 (-1 at the end) ------------------------------
-  // OLA = false: groups blockIdx.x, + gridDim.x, ... of consecutive items.  OLA = true: chunk c x band quad
-  // q (unit c nbq + q from the work counter), frames frame0 .. frame0 + nf - 1, items f B + 4 q + g.
-  int c_frame0 = 0, c_nf = 0, c_bin = -1, c_bout = -1, c_bq = 0, c_k = 0;
-  // per-XCD work queues (workgroup b runs on XCD b mod 8): chunk c goes to XCD c mod 8, so the band quads
-  // of one chunk -- the 16-byte pieces of the same output rows -- meet in one L2 and leave it as whole lines
-  const int xcd = (int)(blockIdx.x & (kXcds - 1));
-  auto grab_unit = [&]() -> int {  // wave-uniform: lane 0's fetch-and-add, read back as a scalar
-    int v = 0;
-    if (threadIdx.x == 0) v = atomicAdd(A.ola.counter + xcd, 1);
-    return __builtin_amdgcn_readfirstlane(v);
-  };
-  auto enter_unit = [&](int ux) -> int {
-    const int c = xcd + kXcds * (ux / A.nbq);
-    if (c >= A.ola.nchunks) return -1;
-    c_bq = ux - (ux / A.nbq) * A.nbq;
-    const OlaChunk ch = A.ola.chunks[c];
-    c_frame0 = ch.frame0; c_nf = ch.nf; c_bin = ch.bin; c_bout = ch.bout; c_k = 0;
-    return c_frame0 * A.B + 4 * c_bq;
-  };
+  // ---- group sequence: groups blockIdx.x, + gridDim.x, ... of consecutive items (-1 at the end) ----
   auto next_group = [&](int ibase) -> int {
-    if constexpr (!OLA) {
-      return ibase + 4 * (int)gridDim.x < 4 * ngroups ? ibase + 4 * (int)gridDim.x : -1;
-    } else {
-      if (c_k + 1 < c_nf) {
-        ++c_k;
-        return ibase + A.B;
-      }
-      return enter_unit(grab_unit());
-    }
+    return ibase + 4 * (int)gridDim.x < 4 * ngroups ? ibase + 4 * (int)gridDim.x : -1;
   };
-  int cur;
-  if constexpr (!OLA) cur = (int)blockIdx.x < ngroups ? 4 * (int)blockIdx.x : -1;
-  else cur = enter_unit(grab_unit());
+  int cur = (int)blockIdx.x < ngroups ? 4 * (int)blockIdx.x : -1;
   if (cur >= 0) dma_a(cur);
-  bool qbad = false;  // a feature without a compact code (OLA, ola_store_feature)
   while (cur >= 0) {
     const int ibase = cur;
-    // OLA: the previous frame's ring stores are complete before this frame reads them (same wave, other
-    // lanes; a workgroup-scope release).  The DMA wait of the split-Durbin path below does the same.
-    if constexpr (OLA && !(DM == kDmExt && CB != 0)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     load_r(ibase);
     // Everything below is re-derived per group from opaque copies, so the compiler cannot hoist
     // group-invariant addresses/tables out of the loop (they would stay live through the Durbin phase).
@@ -1063,13 +1018,12 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
     const int H = A.env_nfft >> 1;
     const int TS = (A.env_nfft / 4 + 1 + 15) / 16;
     const int item = ibase + g;
-    const bool valid = item < A.items && (!OLA || 4 * c_bq + g < A.B);
+    const bool valid = item < A.items;
     // ---- phase 1: Levinson-Durbin (features.py:226-228) in registers -------------------------
     double gg;
     if constexpr (DM == kDmExt) {
       if constexpr (CB != 0) {
-        // la[0 .. la_len) = this group's a rows: LDS-DMA copies issued a group ahead (see below); with the
-        // fused OLA this wait also completes the previous frame's ring stores before this frame reads them
+        // la[0 .. la_len) = this group's a rows: LDS-DMA copies issued a group ahead (see below)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       } else {
         const double* ai = A.a_ext + (int64_t)(valid ? item : 0) * A.a_stride;
@@ -1214,26 +1168,6 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
       }
       wave_lds_sync();
     }
-    // the OLA context of this group's frame (wave-uniform; read here, not at the top of the group, so it is
-    // not live through the Durbin and cepstrum phases): its slice, the rows it owns, the previous frame's
-    // coverage, the chunk edges
-    int o_dst = 0, o_src = 0, o_cnt = 0, o_lo = 0, o_hi = 0, o_tail = 0, o_kf = 0, o_bin = -1, o_bout = -1;
-    int o_band0 = 0;
-    int64_t o_row = 0;
-    if constexpr (OLA) {
-      const int o_f = c_frame0 + c_k;
-      const FrameDesc fd = A.ola.frames[o_f];
-      const UttDesc U = A.ola.utts[fd.utt];
-      o_dst = fd.dst; o_src = fd.src; o_cnt = fd.cnt; o_kf = fd.k;
-      // owned rows [lo, hi) within [0, L) (a truncated tail frame's slice may start at or past L, cnt 0)
-      o_lo = fd.k == 0 ? 0 : min(fd.dst, U.L);
-      o_hi = fd.k + 1 < U.F ? min(A.ola.frames[o_f + 1].dst, U.L) : U.L;
-      o_tail = fd.k > 0 ? A.ola.frames[o_f - 1].dst + A.ola.frames[o_f - 1].cnt : 0;
-      o_row = U.out_row;
-      o_bin = c_k == 0 ? c_bin : -1;
-      o_bout = c_k + 1 == c_nf ? c_bout : -1;
-      o_band0 = 4 * c_bq;
-    }
     cur = next_group(ibase);
     if (cur >= 0) dma_a(cur);  // la is free until the next group
     // ---- phase 3: weights + envelope (computeFDLPSpectrogram.py:194-205) ---------------------
@@ -1266,41 +1200,11 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
       }
     }
     wave_lds_sync();
-    // every envelope sample env[s] of this lane's item goes through emit: to env (OLA = false, or the debug
-    // copy), and with OLA to the output row t = dst + s - src it falls on (owned by this frame: with the
-    // previous frame's tail; the next frame's rows: into the ring or fb; a chunk's first overlap rows: fa)
+    // every envelope sample env[s] of this lane's item goes through emit
     const int kk = A.kk;
     double* const envp = A.env ? A.env + (int64_t)(valid ? item : 0) * kk : nullptr;
-    double* ringr = nullptr;
-    double* ringw = nullptr;
-    if constexpr (OLA) {
-      ringr = A.ola.ring + (int64_t)blockIdx.x * 8 * kk + (o_kf & 1) * 4 * kk + g * kk;
-      ringw = A.ola.ring + (int64_t)blockIdx.x * 8 * kk + ((o_kf + 1) & 1) * 4 * kk + g * kk;
-    }
-    const int64_t obase = o_row * A.B + o_band0 + g;  // output index of (row 0, this item's band)
     auto emit = [&](int s_, double e) {
-      if (!valid) return;
-      if (envp) envp[s_] = e;
-      if constexpr (OLA) {
-        if (s_ < o_src || s_ >= o_src + o_cnt) return;
-        const int t = o_dst + s_ - o_src;
-        const int band = o_band0 + g;
-        if (t >= o_hi) {  // the next frame's row: its tail
-          FDLP_CHECK(t - o_hi < kk);
-          if (o_bout >= 0) A.ola.fb[((int64_t)o_bout * A.B + band) * kk + (t - o_hi)] = e;
-          else ringw[t - o_hi] = e;
-          return;
-        }
-        FDLP_CHECK(t >= o_lo && t - o_dst < kk);
-        if (o_bin >= 0 && t < o_tail) {  // chunk edge: the second half of a boundary row
-          A.ola.fa[((int64_t)o_bin * A.B + band) * kk + (t - o_dst)] = e;
-          return;
-        }
-        double acc = 0.0;  // out[t] = 0, += the frames covering t in frame order (:219-225)
-        if (t < o_tail) acc = acc + ringr[t - o_dst];
-        acc = acc + e;
-        ola_store_feature(acc, obase + t * A.B, A.ola.out, A.ola.out64, A.ola.outq, A.decimals, A.scale10, qbad);
-      }
+      if (valid && envp) envp[s_] = e;
     };
     bool env_done = false;
     if constexpr (CB < 0) {
@@ -1356,51 +1260,9 @@ __global__ __launch_bounds__(64, lat_waves<CB>()) void lpc_env_lattice_kernel(Lp
         }
       }
     }
-    if constexpr (OLA) {
-      // owned rows no sample of this frame falls on ([lo, dst) of a first frame; past dst + cnt of a short
-      // last frame, the dead tail): the previous frame's tail or nothing, i.e. 0 -> log(1e-14)
-      if (valid) {
-        const int band = o_band0 + g;
-        auto rest = [&](int t) {
-          if (o_bin >= 0 && t < o_tail) {  // (not reached: chunk edges sit between full middle frames)
-            A.ola.fa[((int64_t)o_bin * A.B + band) * kk + (t - o_dst)] = 0.0;
-            return;
-          }
-          double acc = 0.0;
-          if (t < o_tail) acc = acc + ringr[t - o_dst];
-          ola_store_feature(acc, obase + t * A.B, A.ola.out, A.ola.out64, A.ola.outq, A.decimals, A.scale10, qbad);
-        };
-        for (int t = o_lo + l; t < min(o_dst, o_hi); t += 16) rest(t);
-        for (int t = max(o_dst + o_cnt, o_lo) + l; t < o_hi; t += 16) rest(t);
-      }
-    }
-  }
-  if constexpr (OLA) {
-    if (qbad) *A.ola.qflag = 1u;
   }
 }
 
-// The overlap rows of a chunk edge inside an utterance (lpc_env_lattice_kernel<..., OLA = true>): the first
-// frame's tail (fb) and the second frame's head (fa), added in the reference's frame order, 0 + fb + fa.
-__global__ __launch_bounds__(256) void ola_fixup_kernel(const OlaBound* __restrict__ bounds, const double* __restrict__ fa,
-                                                        const double* __restrict__ fb, int B, int kk,
-                                                        float* __restrict__ out, double* __restrict__ out64,
-                                                        int16_t* __restrict__ outq, uint32_t* __restrict__ qflag,
-                                                        int decimals, double scale10) {
-  const int b = blockIdx.x;
-  const OlaBound bd = bounds[b];
-  bool bad = false;
-  for (int q = threadIdx.x; q < bd.len * B; q += blockDim.x) {
-    const int r = q / B, band = q - r * B;
-    FDLP_CHECK(r < kk);
-    const int64_t i = ((int64_t)b * B + band) * kk + r;
-    double acc = 0.0;
-    acc = acc + fb[i];
-    acc = acc + fa[i];
-    ola_store_feature(acc, (bd.row0 + r) * B + band, out, out64, outq, decimals, scale10, bad);
-  }
-  if (bad) *qflag = 1u;
-}
 template <int TS>
 __global__ __launch_bounds__(64) void lpc_env_kernel(LpcEnvArgs A) {
   extern __shared__ double sh[];
@@ -1535,6 +1397,7 @@ static hipError_t launch_lpc_env_t(const LpcEnvArgs& A, size_t lds, hipStream_t 
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)lpc_env_kernel<TS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((lpc_env_kernel<TS>), dim3((A.items + 3) / 4), dim3(64), lds, s, A);
+  (void)kmark(kKLpcLds, s);
   return hipGetLastError();
 }
 
@@ -1647,11 +1510,8 @@ hipError_t prepare_lpc_env(DevConsts& c) {
       c.lpc_astride = (std::max({CB != 0 ? lattice_la_len(c, CB, SL) : c.p + 1, 8 * durbin8_sl8(c.p),
                                  durbin4_fits(c) ? 4 * kDurbin4SL : 0}) + 15) / 16 * 16;
     if (lds > 65536) {
-      hipError_t a = hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL, CB, CT>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (a == hipSuccess)
-        a = hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL, CB, CT, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      const hipError_t a = hipFuncSetAttribute((const void*)lpc_env_lattice_kernel<SL, CB, CT>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (a != hipSuccess) return a;
     }
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lpc_env_lattice_kernel<SL, CB, CT>, 64, lds);
@@ -1662,23 +1522,11 @@ hipError_t prepare_lpc_env(DevConsts& c) {
   return hipSuccess;
 }
 
-bool lpc_env_can_fuse(const DevConsts& c) { return c.lpc_blocks > 0; }
-
 hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int items, double* env,
                           double* a_out, double* gg_out, double* cep_out, double* a_ws, double* gg_ws,
-                          hipStream_t s, const OlaFused* ola) {
+                          hipStream_t s) {
   if (items <= 0) return hipSuccess;
-  if (ola && (!lpc_env_can_fuse(c) || !ola->counter || !ola->ring || !ola->chunks || (ola->nbounds > 0 &&
-              (!ola->fa || !ola->fb || !ola->bounds)) || (ola->outq && (ola->decimals < 0 || !ola->qflag))))
-    return hipErrorInvalidValue;
   LpcEnvArgs A;
-  A.B = c.B;
-  A.nbq = (c.B + 3) / 4;
-  A.nunits = ola ? ola->nchunks * A.nbq : 0;
-  A.decimals = ola ? ola->decimals : -1;
-  A.scale10 = 1.0;
-  for (int i = 0; i < A.decimals; ++i) A.scale10 *= 10.0;  // as launch_ola_log
-  A.ola = ola ? *ola : OlaFused{};
   A.a_ext = nullptr;
   A.gg_ext = nullptr;
   A.a_stride = 0;
@@ -1689,11 +1537,13 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
       if (c.lpc_astride < 4 * kDurbin4SL) return hipErrorInvalidValue;
       hipLaunchKernelGGL((durbin4_kernel<kDurbin4SL>), dim3((items + 15) / 16), dim3(64), 0, s, r, c.nlags, c.p, items,
                          a_ws, gd, c.lpc_astride);
+      (void)kmark(kKDurbin4, s);
       return hipGetLastError();
     }() : durbin8_dispatch(c.p, [&](auto sl8) -> hipError_t {
       constexpr int SL8 = decltype(sl8)::value;
       hipLaunchKernelGGL((durbin8_kernel<SL8>), dim3((items + 7) / 8), dim3(64), 0, s, r, c.nlags, c.p, items, a_ws, gd,
                          c.lpc_astride);
+      (void)kmark(kKDurbin8, s);
       return hipGetLastError();
     });
     if (e != hipSuccess) return e;
@@ -1713,29 +1563,19 @@ hipError_t launch_lpc_env(const DevConsts& c, int odd_zero, const double* r, int
   A.r = r; A.weights = c.weights; A.env_cos = c.env_cos; A.env_win = c.env_win; A.env = env;
   A.a_out = a_out; A.gg_out = gg_out; A.cep_out = cep_out;
   if (c.lpc_blocks > 0) {  // lattice Durbin in registers, persistent grid (prepare_lpc_env)
-    // fused OLA: every resident wave takes units from the counter (its ring slot is blockIdx.x)
-    const int grid = ola ? std::min(xcd_grid(A.nunits), c.lpc_blocks) : std::min((items + 3) / 4, c.lpc_blocks);
-    if (ola) {
-      const hipError_t e = hipMemsetAsync(ola->counter, 0, sizeof(int) * kXcds, s);
-      if (e != hipSuccess) return e;
-      if (grid <= 0) return hipSuccess;
-    }
+    const int grid = std::min((items + 3) / 4, c.lpc_blocks);
     const hipError_t e = lattice_dispatch(c, [&](auto sl, auto cb, auto ct) -> hipError_t {
       constexpr int SL = decltype(sl)::value, CB = decltype(cb)::value;
       constexpr int CT = decltype(ct)::value;
       const size_t lds = lattice_lds(c, CB, SL);
       A.region = lattice_region(c, CB, SL);
       A.la_len = CB != 0 ? lattice_la_len(c, CB, SL) : 0;
-      if (ola) hipLaunchKernelGGL((lpc_env_lattice_kernel<SL, CB, CT, true>), dim3(grid), dim3(64), lds, s, A);
-      else hipLaunchKernelGGL((lpc_env_lattice_kernel<SL, CB, CT>), dim3(grid), dim3(64), lds, s, A);
+      hipLaunchKernelGGL((lpc_env_lattice_kernel<SL, CB, CT>), dim3(grid), dim3(64), lds, s, A);
+      (void)kmark(kKLattice, s);
       return hipGetLastError();
     });
-    if (e != hipSuccess || !ola || ola->nbounds == 0) return e;
-    hipLaunchKernelGGL(ola_fixup_kernel, dim3(ola->nbounds), dim3(256), 0, s, ola->bounds, ola->fa, ola->fb, c.B, c.kk,
-                       ola->out, ola->out64, ola->outq, ola->qflag, A.decimals, A.scale10);
-    return hipGetLastError();
+    return e;
   }
-  if (ola) return hipErrorInvalidValue;
   const size_t lds = sizeof(double) * (4 * (size_t)A.region);
   switch ((c.env_nfft / 4 + 1 + 15) / 16) {  // envelope slots: u = 0 .. env_nfft/4
 #define FDLP_TS_CASE(n) case n: return launch_lpc_env_t<n>(A, lds, s);

@@ -122,10 +122,14 @@ hipError_t launch_ola_log(const DevConsts& c, const double* env, const FrameDesc
   for (int i = 0; i < decimals; ++i) scale10 *= 10.0;
   dim3 grid((unsigned)((maxL + kOlaRows - 1) / kOlaRows), n_utt);
   const size_t lds = sizeof(double) * kOlaRows * (size_t)(c.B + 1);
-  if (lds > 65536)
+  // the kernel's static LDS (log table, frame range) counts against the same 64 KB default limit
+  constexpr size_t kStaticLds = sizeof(double) * 3 * kLogTab + 2 * sizeof(int);
+  if (lds + kStaticLds > 160 * 1024) return hipErrorInvalidValue;  // B > ~620 bands: no tile fits a CU
+  if (lds + kStaticLds > 65536)
     (void)hipFuncSetAttribute((const void*)ola_log_tiled_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(ola_log_tiled_kernel, grid, dim3(256), lds, s, c, env, frames, utts, out, out_f64, out_q, q_flag,
                      decimals, scale10);
+  (void)kmark(kKOlaLog, s);
   return hipGetLastError();
 }
 

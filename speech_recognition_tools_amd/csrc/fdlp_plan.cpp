@@ -398,17 +398,7 @@ struct fdlp_plan {
   hipEvent_t staging_done = nullptr;
   bool staging_pending = false;
   int last_frames = 0;
-  // fused OLA (fdlp_set_ola_path; lpc_env_lattice_kernel<..., OLA>): chunk / boundary tables (pinned staging
-  // + device), the work counter, the per-wave tail ring, the boundary halves (grown on demand)
-  int ola_path = FDLP_OLA_AUTO;
-  int ola_last = 0;                  // the OLA the last fdlp_compute ran (FDLP_OLA_FUSED / _SEPARATE)
   bool env_valid = false;            // ws.env holds the last batch's envelopes (fdlp_debug_fetch)
-  fdlp::OlaChunk *h_chunks = nullptr, *d_chunks = nullptr;
-  fdlp::OlaBound *h_bounds = nullptr, *d_bounds = nullptr;
-  int* d_ola_counter = nullptr;
-  double* d_ola_ring = nullptr;
-  double* d_ola_fab = nullptr;       // fa then fb, [2][cap][B][kk]
-  size_t ola_fab_cap = 0;            // boundaries
   // optional per-stage HIP-event timing (fdlp_set_profiling / fdlp_stage_times)
   bool profiling = false;
   bool debug_intermediates = false;  // keep a/gg/cep of the fused LPC kernel for fdlp_debug_fetch
@@ -434,15 +424,56 @@ struct fdlp_plan {
   std::vector<std::vector<hipEvent_t>> prof_pending;
   double prof_ms[FDLP_NUM_STAGES] = {0};
   int prof_calls = 0;
+  // per-kernel marks (profiling level 2): per call, the start event then one mark per kernel (one stream)
+  bool kprofiling = false;
+  std::vector<std::vector<fdlp::KMark>> kmark_pending;
+  double kern_ms[FDLP_NUM_KERNELS] = {0};
+  int64_t kern_launches[FDLP_NUM_KERNELS] = {0};
 };
 
 // the recipes' DCT as one kernel per frame (dct_frame_kernel) unless fdlp_set_dct_path chose the
+namespace fdlp {
+thread_local std::vector<KMark>* g_kmarks = nullptr;
+hipError_t kmark(int id, hipStream_t s) {
+  if (!g_kmarks) return hipSuccess;
+  const hipError_t le = hipPeekAtLastError();  // a failed launch stays the caller's hipGetLastError()
+  if (le != hipSuccess) return le;
+  hipEvent_t ev = nullptr;
+  hipError_t e = hipEventCreate(&ev);
+  if (e == hipSuccess) e = hipEventRecord(ev, s);
+  if (e != hipSuccess) {
+    if (ev) (void)hipEventDestroy(ev);
+    return e;
+  }
+  g_kmarks->push_back(KMark{id, ev});
+  return hipSuccess;
+}
+}  // namespace fdlp
+
 // two four-step kernels
 static bool dct_fused(const fdlp_plan* p) { return p->dc.dct1_tw && p->dct_path == FDLP_DCT_AUTO; }
 
 namespace {
 
+int drain_kmarks(fdlp_plan* p) {
+  for (auto& v : p->kmark_pending) {
+    if (!v.empty()) HIP_TRY(hipEventSynchronize(v.back().ev));
+    for (size_t i = 1; i < v.size(); ++i) {
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, v[i - 1].ev, v[i].ev));
+      const int id = v[i].id >= 0 && v[i].id < FDLP_NUM_KERNELS ? v[i].id : fdlp::kKOther;
+      p->kern_ms[id] += ms;
+      p->kern_launches[id]++;
+    }
+    for (auto& m : v) (void)hipEventDestroy(m.ev);
+  }
+  p->kmark_pending.clear();
+  return FDLP_OK;
+}
+
 int drain_profile(fdlp_plan* p) {
+  const int krc = drain_kmarks(p);
+  if (krc != FDLP_OK) return krc;
   // per call: 5 events per sub-batch (stage 0..3 boundaries on its stream) + 2 around the OLA
   for (auto& ev : p->prof_pending) {
     HIP_TRY(hipEventSynchronize(ev.back()));
@@ -467,17 +498,17 @@ int free_plan(fdlp_plan* p) {
   if (!p) return FDLP_OK;
   for (auto& ev : p->prof_pending)
     for (auto e : ev) (void)hipEventDestroy(e);
+  for (auto& v : p->kmark_pending)
+    for (auto& m : v) (void)hipEventDestroy(m.ev);
   void* devs[] = {p->d_fbank, p->d_hamming, p->d_weights, p->d_env_cos, p->d_env_win, p->d_tw1, p->d_post, p->d_rtw,
                   p->d_om1, p->d_om2, p->d_dct1, p->d_lo, p->d_hi, p->ws.z, p->ws.dct, p->ws.r, p->ws.a, p->ws.gg,
                   p->ws.cep, p->ws.env, p->ws.a_pad, p->d_frames, p->d_utts, p->d_sk_e, p->r_up, p->d_sk_snap,
                   p->d_sk_reg, p->d_faxis, p->r_flat, p->d_fl_ev, p->r_flat_part, p->d_fl_band, p->d_sk_wrap,
-                  p->r_wrap, p->d_chunks, p->d_bounds, p->d_ola_counter, p->d_ola_ring, p->d_ola_fab};
+                  p->r_wrap};
   for (void* d : devs)
     if (d) (void)hipFree(d);
   if (p->h_frames) (void)hipHostFree(p->h_frames);
   if (p->h_utts) (void)hipHostFree(p->h_utts);
-  if (p->h_chunks) (void)hipHostFree(p->h_chunks);
-  if (p->h_bounds) (void)hipHostFree(p->h_bounds);
   if (p->staging_done) (void)hipEventDestroy(p->staging_done);
   if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
   if (p->ev_join) (void)hipEventDestroy(p->ev_join);
@@ -538,55 +569,6 @@ int ola_table(const fdlp_plan* p, int F, int L, const uint8_t* jit, int32_t* dst
     else ptr = ptr + p->ola_hop + (jit ? jit[i - 1] : 0);
   }
   return FDLP_OK;
-}
-
-// Fused OLA tables of a batch (lpc_env_lattice_kernel<..., OLA>, fdlp_internal.h OlaChunk): one chunk per
-// utterance, cut every kOlaChunk frames between two middle frames (full kk, src 0, overlapping) while at least
-// three frames remain, so no chunk runs much longer than the others; chunks sorted longest first for the work
-// counter.  Returns false (the separate OLA kernel runs) when a row would be covered by more than two frames
-// (the fused sum keeps only the previous frame's tail) or the tables do not fit.
-constexpr int kOlaChunk = 8;
-bool build_ola_chunks(fdlp_plan* p, int n_utt, int* nchunks, int* nbounds) {
-  const fdlp::FrameDesc* fr = p->h_frames;
-  const int kk = p->kk;
-  std::vector<fdlp::OlaChunk> ch;
-  int nb = 0;
-  for (int u = 0; u < n_utt; ++u) {
-    const fdlp::UttDesc& U = p->h_utts[u];
-    const fdlp::FrameDesc* f = fr + U.frame0;
-    if (U.F > 0 && f[0].dst != 0) return false;
-    for (int k = 1; k + 1 < U.F; ++k)  // frame k + 1 starts where frame k - 1 ends or later
-      if (f[k + 1].dst < f[k - 1].dst + f[k - 1].cnt) return false;
-    int k0 = 0;
-    int bin = -1;
-    while (k0 < U.F) {
-      int k1 = U.F;  // chunk [k0, k1)
-      int bout = -1;
-      for (int kb = k0 + kOlaChunk; kb + 3 <= U.F; ++kb) {  // the first valid cut at or after k0 + kOlaChunk
-        const fdlp::FrameDesc &a = f[kb - 1], &b = f[kb];
-        const int len = a.dst + kk - b.dst;
-        if (a.cnt == kk && b.cnt == kk && a.src == 0 && b.src == 0 && len > 0 && len <= kk && kb - 1 >= 1) {
-          if (nb >= p->max_frames) return false;
-          fdlp::OlaBound& bd = p->h_bounds[nb];
-          bd.row0 = U.out_row + b.dst;
-          bd.len = len;
-          bd.pad = 0;
-          bout = nb++;
-          k1 = kb;
-          break;
-        }
-      }
-      ch.push_back(fdlp::OlaChunk{U.frame0 + k0, k1 - k0, bin, bout});
-      bin = bout;
-      k0 = k1;
-    }
-  }
-  if ((int)ch.size() > p->max_frames) return false;
-  std::stable_sort(ch.begin(), ch.end(), [](const fdlp::OlaChunk& x, const fdlp::OlaChunk& y) { return x.nf > y.nf; });
-  std::copy(ch.begin(), ch.end(), p->h_chunks);
-  *nchunks = (int)ch.size();
-  *nbounds = nb;
-  return true;
 }
 
 }  // namespace
@@ -891,14 +873,6 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
       hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&p->aux_stream, hipStreamNonBlocking) != hipSuccess)
     PLAN_FAIL(FDLP_E_NOMEM, "workspace allocation failed (reduce max_frames)");
-  if (!p->modspec && fdlp::lpc_env_can_fuse(d) &&
-      (hipMalloc((void**)&p->d_chunks, sizeof(fdlp::OlaChunk) * F) != hipSuccess ||
-       hipMalloc((void**)&p->d_bounds, sizeof(fdlp::OlaBound) * F) != hipSuccess ||
-       hipHostMalloc((void**)&p->h_chunks, sizeof(fdlp::OlaChunk) * F, hipHostMallocDefault) != hipSuccess ||
-       hipHostMalloc((void**)&p->h_bounds, sizeof(fdlp::OlaBound) * F, hipHostMallocDefault) != hipSuccess ||
-       hipMalloc((void**)&p->d_ola_counter, sizeof(int) * fdlp::kXcds) != hipSuccess ||
-       hipMalloc((void**)&p->d_ola_ring, sizeof(double) * 8 * (size_t)p->kk * (size_t)d.lpc_blocks) != hipSuccess))
-    PLAN_FAIL(FDLP_E_NOMEM, "workspace allocation failed (fused OLA tables)");
   phase(3);
 #undef PLAN_FAIL
 #undef PLAN_TRY
@@ -1042,48 +1016,11 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
   // Sub-batches alternate between the caller's stream and the plan's second stream so that the
   // MFMA-bound autocorrelation of one overlaps the VALU-bound DFT / LPC kernels of the other.
   const int nsub = (int)std::max<int64_t>(1, std::min<int64_t>(p->pipeline, nf / 256));
-  // OLA + log fused into the LPC kernel on request (fdlp_set_ola_path(FUSED); the envelopes never go to HBM)
-  // unless sub-batches, the modulation spectrum or the LDS Durbin rule it out
-  int ola_nchunks = 0, ola_nbounds = 0;
-  const bool fuse = !p->modspec && p->ola_path == FDLP_OLA_FUSED && nsub == 1 && p->h_chunks &&
-                    fdlp::lpc_env_can_fuse(p->dc) && build_ola_chunks(p, b->n_utt, &ola_nchunks, &ola_nbounds);
-  if (fuse && (size_t)ola_nbounds > p->ola_fab_cap) {
-    if (p->d_ola_fab) HIP_TRY(hipFree(p->d_ola_fab));  // (the device is idle on it: staging_done waited above)
-    p->d_ola_fab = nullptr;
-    p->ola_fab_cap = 0;
-    const size_t cap = std::max<size_t>(ola_nbounds, 64);
-    HIP_TRY(hipMalloc((void**)&p->d_ola_fab, sizeof(double) * 2 * cap * p->B * p->kk));
-    p->ola_fab_cap = cap;
-  }
   HIP_TRY(hipMemcpyAsync(p->d_frames, p->h_frames, sizeof(fdlp::FrameDesc) * nf, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(p->d_utts, p->h_utts, sizeof(fdlp::UttDesc) * b->n_utt, hipMemcpyHostToDevice, s));
-  if (fuse) {
-    HIP_TRY(hipMemcpyAsync(p->d_chunks, p->h_chunks, sizeof(fdlp::OlaChunk) * ola_nchunks, hipMemcpyHostToDevice, s));
-    if (ola_nbounds)
-      HIP_TRY(hipMemcpyAsync(p->d_bounds, p->h_bounds, sizeof(fdlp::OlaBound) * ola_nbounds, hipMemcpyHostToDevice, s));
-  }
   HIP_TRY(hipEventRecord(p->staging_done, s));
   p->staging_pending = true;
-  p->ola_last = p->modspec ? 0 : (fuse ? FDLP_OLA_FUSED : FDLP_OLA_SEPARATE);
-  p->env_valid = !p->modspec && (!fuse || p->debug_intermediates);
-  fdlp::OlaFused ola{};
-  if (fuse) {
-    ola.frames = p->d_frames;
-    ola.utts = p->d_utts;
-    ola.chunks = p->d_chunks;
-    ola.bounds = p->d_bounds;
-    ola.nchunks = ola_nchunks;
-    ola.nbounds = ola_nbounds;
-    ola.counter = p->d_ola_counter;
-    ola.ring = p->d_ola_ring;
-    ola.fa = p->d_ola_fab;
-    ola.fb = p->d_ola_fab ? p->d_ola_fab + p->ola_fab_cap * p->B * p->kk : nullptr;
-    ola.out = b->out_dev;
-    ola.out64 = b->out_f64_dev;
-    ola.outq = b->out_q_dev;
-    ola.qflag = b->out_q_flag_dev;
-    ola.decimals = b->ark_decimals;
-  }
+  p->env_valid = !p->modspec;
 
   std::vector<hipEvent_t> ev;
   if (p->profiling) {
@@ -1094,6 +1031,25 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     ev.resize(5 * (size_t)nsub + 2);
     for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
   }
+  // per-kernel marks (one sub-batch: every kernel on stream s): a start event, then one per kernel launch
+  std::vector<fdlp::KMark> kmarks;
+  const bool kprof = p->profiling && p->kprofiling && nsub == 1;
+  if (kprof) {
+    hipEvent_t e0 = nullptr;
+    HIP_TRY(hipEventCreate(&e0));
+    kmarks.push_back(fdlp::KMark{-1, e0});
+    HIP_TRY(hipEventRecord(e0, s));
+    fdlp::g_kmarks = &kmarks;
+  }
+  struct KmarkScope {  // an early error return: stop collecting and free the marks of this call
+    bool on;
+    std::vector<fdlp::KMark>& v;
+    ~KmarkScope() {
+      if (!on) return;
+      fdlp::g_kmarks = nullptr;
+      for (auto& m : v) (void)hipEventDestroy(m.ev);
+    }
+  } kscope{kprof, kmarks};
   // frames [f0, f0 + n) of sub-batch i: everything up to the envelopes is independent per frame
   auto run_frames = [&](int i, int64_t f0, int n, hipStream_t st) -> int {
     auto mark = [&](int k) -> hipError_t { return p->profiling ? hipEventRecord(ev[5 * i + k], st) : hipSuccess; };
@@ -1101,7 +1057,7 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     const size_t it0 = (size_t)f0 * B;
     const int its = n * p->B;
     double* r = p->ws.r + it0 * nl;
-    double* env = fuse && !p->debug_intermediates ? nullptr : p->ws.env + it0 * p->kk;  // fused: debug copy only
+    double* env = p->ws.env + it0 * p->kk;
     double* a_dbg = p->debug_intermediates ? p->ws.a + it0 * (p->p + 1) : nullptr;
     double* gg_dbg = p->debug_intermediates ? p->ws.gg + it0 : nullptr;
     double* cep_dbg = (p->debug_intermediates || p->modspec) ? p->ws.cep + it0 * p->M : nullptr;
@@ -1142,7 +1098,7 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     HIP_TRY(mark(3));
     HIP_TRY(fdlp::launch_lpc_env(p->dc, p->cfg.odd_mod_zero, r, its, env, a_dbg, gg_dbg, cep_dbg,
                                   p->ws.a_pad ? p->ws.a_pad + it0 * p->dc.lpc_astride : nullptr, p->ws.gg + it0,
-                                  st, fuse ? &ola : nullptr));
+                                  st));
     HIP_TRY(mark(4));
     return FDLP_OK;
   };
@@ -1167,13 +1123,18 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     HIP_TRY(fdlp::launch_modspec_out(p->ws.cep, p->d_frames, p->d_utts, (int)nf, p->B, p->M, c.coeff_0 - 1,
                                      p->feat_len, c.keep_even ? 2 : 1, keep_odd_slot, p->d_faxis,
                                      c.absolute_value, b->out_dev, b->out_f64_dev, b->ark_decimals, s));
-  } else if (!p->modspec && !fuse) {  // (complex modulation: launch_cplx_modspec; fused: the LPC kernel)
+  } else if (!p->modspec) {  // (complex modulation: launch_cplx_modspec)
     HIP_TRY(fdlp::launch_ola_log(p->dc, p->ws.env, p->d_frames, p->d_utts, b->n_utt, maxL, b->out_dev,
                                  b->out_f64_dev, b->out_q_dev, b->out_q_flag_dev, b->ark_decimals, s));
   }
   if (p->profiling) {
     HIP_TRY(hipEventRecord(ev.back(), s));
     p->prof_pending.push_back(ev);
+  }
+  if (kprof) {
+    fdlp::g_kmarks = nullptr;
+    p->kmark_pending.push_back(kmarks);
+    kmarks.clear();  // owned by kmark_pending now
   }
   return FDLP_OK;
 }
@@ -1252,18 +1213,6 @@ int fdlp_dct_path(const fdlp_plan* p) {
   return dct_fused(p) ? FDLP_DCT_FRAME : FDLP_DCT_FOUR_STEP;
 }
 
-int fdlp_set_ola_path(fdlp_plan* p, int32_t path) {
-  if (!p || (path != FDLP_OLA_AUTO && path != FDLP_OLA_SEPARATE && path != FDLP_OLA_FUSED))
-    return fail(FDLP_E_INVALID, "fdlp_set_ola_path: FDLP_OLA_AUTO, FDLP_OLA_SEPARATE or FDLP_OLA_FUSED");
-  p->ola_path = path;
-  return FDLP_OK;
-}
-
-int fdlp_ola_path(const fdlp_plan* p) {
-  if (!p) return fail(FDLP_E_INVALID, "fdlp_ola_path: null plan");
-  return p->ola_last;
-}
-
 int fdlp_set_pipeline(fdlp_plan* p, int32_t n_sub) {
   if (!p || n_sub < 1) return fail(FDLP_E_INVALID, "fdlp_set_pipeline: need a plan and n_sub >= 1");
   p->pipeline = n_sub;
@@ -1313,9 +1262,32 @@ int fdlp_set_profiling(fdlp_plan* p, int32_t enable) {
   int rc = drain_profile(p);
   if (rc != FDLP_OK) return rc;
   p->profiling = enable != 0;
+  p->kprofiling = enable >= 2;
   for (double& v : p->prof_ms) v = 0.0;
   p->prof_calls = 0;
+  for (double& v : p->kern_ms) v = 0.0;
+  for (int64_t& v : p->kern_launches) v = 0;
   return FDLP_OK;
+}
+
+int fdlp_kernel_times(fdlp_plan* p, double* ms_sum, int64_t* launches) {
+  if (!p || !ms_sum) return fail(FDLP_E_INVALID, "fdlp_kernel_times: bad args");
+  int rc = drain_profile(p);
+  if (rc != FDLP_OK) return rc;
+  for (int k = 0; k < FDLP_NUM_KERNELS; ++k) {
+    ms_sum[k] = p->kern_ms[k];
+    if (launches) launches[k] = p->kern_launches[k];
+  }
+  return FDLP_OK;
+}
+
+const char* fdlp_kernel_name(int32_t id) {
+  static const char* const names[FDLP_NUM_KERNELS] = {
+      "fdlp::dct_frame_kernel", "fdlp::frames_dft1", "fdlp::dft2_dct", "fdlp::ac_vsweep_kernel<skirts>",
+      "fdlp::ac_vsweep_kernel<flat>", "fdlp::ac_wrap_kernel", "fdlp::ac_band_kernel", "fdlp::ac_sweep_kernel",
+      "fdlp::autocorr_kernel", "fdlp::durbin4_kernel", "fdlp::durbin8_kernel", "fdlp::lpc_env_lattice_kernel",
+      "fdlp::lpc_env_kernel", "fdlp::ola_log_tiled_kernel", "other", ""};
+  return id >= 0 && id < FDLP_NUM_KERNELS ? names[id] : "";
 }
 
 int fdlp_stage_times(fdlp_plan* p, double* ms_sum, int32_t* n_calls) {
@@ -1338,8 +1310,7 @@ int fdlp_debug_fetch_range(fdlp_plan* p, int32_t f0, int32_t n, double* dct, dou
   if ((a && !p->ws.a) || (cep && !p->ws.cep))
     return fail(FDLP_E_INVALID, "fdlp_debug_fetch: a / cep are kept only after fdlp_set_debug(plan, 1)");
   if (env && !p->env_valid)
-    return fail(FDLP_E_INVALID, "fdlp_debug_fetch: with the fused OLA the envelopes are kept only after "
-                                "fdlp_set_debug(plan, 1)");
+    return fail(FDLP_E_INVALID, "fdlp_debug_fetch: no envelopes (modulation-spectrum plan or no compute yet)");
   if (dct) HIP_TRY(hipMemcpy(dct, p->ws.dct + (size_t)f0 * p->N, sizeof(double) * n * (size_t)p->N, hipMemcpyDeviceToHost));
   if (r) HIP_TRY(hipMemcpy(r, p->ws.r + it0 * p->nlags, sizeof(double) * items * p->nlags, hipMemcpyDeviceToHost));
   if (a) HIP_TRY(hipMemcpy(a, p->ws.a + it0 * (p->p + 1), sizeof(double) * items * (p->p + 1), hipMemcpyDeviceToHost));

@@ -256,6 +256,8 @@ def _run_native(args, cfg, device, noise, snr, diff):
     o.out_codes = {'auto': -1, 'on': 1, 'off': 0}[getattr(args, 'd2h_codes', 'auto')]
     o.chunk_rows = int(getattr(args, 'chunk_rows', 0) or 0)
     o.keep_warm = int(bool(getattr(args, 'keep_warm', False)))
+    if o.keep_warm:
+        _register_job_release()
     trace = getattr(args, 'job_trace', None)
     o.trace_path = trace.encode() if trace else None
     st = _lib.FdlpJobStatsC()
@@ -285,13 +287,29 @@ def _run_native(args, cfg, device, noise, snr, diff):
     return None
 
 
+_RELEASE_REGISTERED = False
+
+
+def _register_job_release():
+    """--keep_warm parks the plan, streams and pinned slots in the library; include/fdlp.h asks for
+    fdlp_job_release before the HIP runtime is torn down, so the process releases them at exit."""
+    global _RELEASE_REGISTERED
+    if _RELEASE_REGISTERED:
+        return
+    import atexit
+    from speech_recognition_tools_amd import _lib
+    atexit.register(_lib.lib.fdlp_job_release)
+    _RELEASE_REGISTERED = True
+
+
 LAST_JOB_STATS = None  # fdlp_job_stats of the last native run (benchmarks/cli_throughput.py reports it)
 
 
 def main(argv=None):
     from speech_recognition_tools_amd.featgen import _early_hip
-    args = build_parser().parse_args(argv)
     try:
+        # inside the try: a usage error (SystemExit 2) still joins the helper thread first
+        args = build_parser().parse_args(argv)
         if native_eligible(args) and "torch" not in sys.modules:
             from speech_recognition_tools_amd import _hip_runtime
             _hip_runtime.TORCH = False  # before anything loads libfdlp_hip.so: a cold JOB skips importing torch

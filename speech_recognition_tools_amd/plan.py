@@ -215,21 +215,6 @@ class FdlpPlan:
         check(lib.fdlp_plan_flat_events(self._h, None, None, ctypes.byref(n), ptr(ev, ctypes.c_int32), n.value))
         return C.value, H.value, ev
 
-    OLA_PATHS = {"auto": 0, "separate": 1, "fused": 2}
-
-    def set_ola_path(self, path: str = "auto"):
-        """'auto' / 'separate': ola_log_tiled_kernel after the LPC kernel; 'fused': OLA + log inside the LPC
-        kernel where it applies (bit-identical; measured slower; fdlp_set_ola_path)."""
-        check(lib.fdlp_set_ola_path(self._h, self.OLA_PATHS[path]))
-
-    @property
-    def ola_path(self) -> Optional[str]:
-        """The OLA stage the last compute ran: 'fused', 'separate' or None (none yet / modulation spectrum)."""
-        v = lib.fdlp_ola_path(self._h)
-        if v < 0:
-            check(v)
-        return {0: None, 1: "separate", 2: "fused"}[v]
-
     def set_pipeline(self, n_sub: int):
         check(lib.fdlp_set_pipeline(self._h, int(n_sub)))
 
@@ -249,8 +234,19 @@ class FdlpPlan:
                                            for k in ("dct", "r", "a", "gg", "cep", "env")]))
         return d
 
-    def set_profiling(self, enable: bool = True):
-        check(lib.fdlp_set_profiling(self._h, int(bool(enable))))
+    def set_profiling(self, enable=True, kernels: bool = False):
+        """Per-stage HIP events on every fdlp_compute; kernels=True also marks every kernel launch
+        (kernel_times)."""
+        check(lib.fdlp_set_profiling(self._h, (2 if kernels else 1) if enable else 0))
+
+    def kernel_times(self):
+        """{kernel name: (summed ms, launches)} of the profiled calls (set_profiling(kernels=True)): the time
+        between consecutive HIP events on the kernels' stream, one kernel each."""
+        ms = np.zeros(_lib.FDLP_NUM_KERNELS, dtype=np.float64)
+        n = np.zeros(_lib.FDLP_NUM_KERNELS, dtype=np.int64)
+        check(lib.fdlp_kernel_times(self._h, ptr(ms, ctypes.c_double), ptr(n, ctypes.c_int64)))
+        return {lib.fdlp_kernel_name(k).decode(): (float(ms[k]), int(n[k]))
+                for k in range(_lib.FDLP_NUM_KERNELS) if n[k] > 0}
 
     def stage_times(self):
         """{stage: summed ms} over the profiled fdlp_compute calls, and the call count."""

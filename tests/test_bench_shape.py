@@ -43,7 +43,6 @@ def _run_batch(entries, cfg_name="wsj", pcm=None, lens=None, mix=None, max_frame
     jit = PyRandom(7).randbits2(nj)
     _, rows, out64 = plan.compute(torch.from_numpy(pcm).cuda(), lens, jit, want_f64=True, **(mix or {}))
     torch.cuda.synchronize()
-    assert plan.ola_path == "separate"
     offs = np.concatenate([[0], np.cumsum(lens)])
     jo = np.concatenate([[0], np.cumsum([g[0] - 1 for g in geo])])
     fo = np.concatenate([[0], np.cumsum([g[0] for g in geo])])

@@ -3,6 +3,7 @@ every JOB gets --device_rr=JOB,<ngpu> so JOB n runs on GPU (n-1) mod ngpu (the r
 the driver with --cmd "$train_cmd", e2e/wsj/run_fdlp_e1.sh:189-209); the CLI resolves it before any GPU
 call.  A fake run.pl records the command lines instead of running them."""
 import os
+import sys
 import subprocess
 
 import pytest
@@ -267,7 +268,7 @@ def test_early_hip_start_narrows_like_main(monkeypatch):
         monkeypatch.delenv(v, raising=False)
     monkeypatch.setattr(_early_hip, "NARROWED", False)
     monkeypatch.setattr(_early_hip, "_thread", None)
-    monkeypatch.setattr(_early_hip, "_warm", lambda: None)  # no HIP runtime start in the CPU suite
+    monkeypatch.setattr(_early_hip, "_warm", lambda dev: None)  # no HIP runtime start in the CPU suite
     had_torch = sys.modules.pop("torch", None)
     try:
         for argv in (["a.scp", "o", "--host_runner=python"], ["a.scp", "o", "--add_reverb=small_room"]):
@@ -281,3 +282,39 @@ def test_early_hip_start_narrows_like_main(monkeypatch):
         if had_torch is not None:
             sys.modules["torch"] = had_torch
         monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+
+
+def test_early_hip_warms_the_jobs_own_device(monkeypatch):
+    """ADVICE r5 / VERDICT r5 item 8: with CUDA_VISIBLE_DEVICES set the visible set is not narrowed, and the
+    helper must warm the GPU main() will use (resolve_device), not device 0; unknown options start nothing
+    (main()'s parse_args exits 2 with no helper inside the HIP runtime start)."""
+    import sys
+    from speech_recognition_tools_amd.featgen import _early_hip
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "LOCAL_RANK"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("CUDA_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
+    had_torch = sys.modules.pop("torch", None)
+    warmed = []
+    monkeypatch.setattr(_early_hip, "_warm", lambda dev: warmed.append(dev))
+    monkeypatch.setattr(_early_hip, "NARROWED", False)
+    monkeypatch.setattr(_early_hip, "_thread", None)
+    try:
+        assert _early_hip.warm_target(["a.scp", "o", "--device_rr", "3,4"]) == (2, False)
+        assert _early_hip.warm_target(["a.scp", "o", "--device", "5"]) == (5, False)
+        assert _early_hip.warm_target(["a.scp", "o", "--bogus_option"]) is None
+        assert _early_hip.warm_target(["a.scp", "o", "--device_rr", "0,4"]) is None  # main() raises it
+        _early_hip.start(["a.scp", "o", "--device_rr", "3,4"])
+        _early_hip.join()
+        assert warmed == [2] and not _early_hip.NARROWED and "HIP_VISIBLE_DEVICES" not in os.environ
+    finally:
+        if had_torch is not None:
+            sys.modules["torch"] = had_torch
+
+
+def test_cli_unknown_option_exits_2_cleanly(tmp_path):
+    """A misspelled option: usage error, exit status 2, and no HIP helper was started."""
+    cli = os.path.join(ROOT, "bin", "compute-fdlp-feats")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="")
+    r = subprocess.run(["bash", cli, "a.scp", str(tmp_path / "o"), "--no_such_option"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "unrecognized arguments" in r.stderr

@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     for name in syms:
         assert hasattr(_lib.lib, name), name
     assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
-    assert _lib.lib.fdlp_abi_version() == 8
+    assert _lib.lib.fdlp_abi_version() == 9
 
 
 @pytest.mark.parametrize("seed", [0, 1, 7, 1234, 2 ** 40 + 5, 2 ** 64 + 3])
