@@ -339,6 +339,15 @@ int fdlp_nprandom_destroy(fdlp_nprandom* rng);
  * energies from int16-wrapped squares exactly like the reference. */
 int fdlp_noise_params(const int16_t* sig, int64_t T, const int16_t* noise, int64_t noise_len,
                       double snr, double u, int64_t* off, double* alpha);
+/* scipy.io.wavfile.read's dtype of a WAV's samples (ABI 9; fdlp_wav_kind): 8-bit PCM -> uint8, 16 -> int16,
+ * 24/32 -> int32 (24-bit left-justified), 40..64 -> int64, IEEE float 32 / 64. */
+enum { FDLP_SIG_U8 = 1, FDLP_SIG_I16 = 2, FDLP_SIG_I32 = 3, FDLP_SIG_I64 = 4, FDLP_SIG_F32 = 5, FDLP_SIG_F64 = 6 };
+/* The same for a signal of any of those dtypes, given as the double values of scipy's array (ABI 9): the
+ * reference squares the signal in its own dtype (integer squares wrap, float32 squares round to float32) and
+ * np.mean sums them like numpy (8192-element chunks, pairwise inside a chunk; float32 accumulated in float32),
+ * features.py:27.  The noise is int16 (noises/*.wav of the recipes). */
+int fdlp_noise_params_any(const double* sig, int64_t T, int32_t sig_kind, const int16_t* noise,
+                          int64_t noise_len, double snr, double u, int64_t* off, double* alpha);
 
 /* ---- native I/O (replaces scipy.io.wavfile.read :139 and dict2Ark + copy-feats :231) ---- */
 /* Parse a RIFF/WAVE PCM16 mono buffer.  *samples points into `buf`. */
@@ -351,6 +360,8 @@ int fdlp_wav_parse(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* cha
  * the double values of scipy's array (ABI 3). */
 int fdlp_wav_decode(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* channels, int32_t* is_int16,
                     int64_t* n_samples, double* out);
+/* FDLP_SIG_* kind of the samples scipy.io.wavfile.read returns for this buffer (ABI 9). */
+int fdlp_wav_kind(const uint8_t* buf, int64_t len, int32_t* kind);
 typedef struct fdlp_ark_writer fdlp_ark_writer;
 /* Kaldi binary ark + scp ("<utt> <abs ark path>:<offset>") like `copy-feats ark,t:- ark,scp:`.  Written to
  * <path>.tmp and renamed to <path> by fdlp_ark_close (removed instead after a failed write). */

@@ -320,7 +320,12 @@ DIFF_KERNEL = np.array([1, 2, 3, 2, 0, -2, -5, -2, 0, 2, 3, 2, 1])   # :163
 
 
 def diff_signal(sig: np.ndarray) -> np.ndarray:
-    """scipy.signal.convolve(sig, a, 'same') on int16 input -> int64 (:162-164)."""
+    """scipy.signal.convolve(sig, a, 'same') (:162-164): integer input (int16 / int32 / uint8) -> int64, exact;
+    float input -> float64 (scipy's direct route for a 13-tap kernel: np.convolve in float64)."""
+    if not np.issubdtype(sig.dtype, np.integer):
+        full = np.convolve(sig.astype(np.float64), DIFF_KERNEL.astype(np.float64))
+        off = (DIFF_KERNEL.size - 1) // 2
+        return full[off:off + sig.size]
     full = np.convolve(sig.astype(np.int64), DIFF_KERNEL)
     off = (DIFF_KERNEL.size - 1) // 2
     return full[off:off + sig.size]
@@ -328,7 +333,8 @@ def diff_signal(sig: np.ndarray) -> np.ndarray:
 
 def noise_mix_params(sig: np.ndarray, noise: np.ndarray, snr: float, u: float):
     """(offset, alpha) of add_noise_to_wav with the draw u = np.random.rand() (features.py:24-29).
-    sig**2 and ns**2 stay int16 (wrap) like the reference."""
+    sig**2 and ns**2 stay in their own dtypes (int16 wraps) like the reference; sig may be any dtype
+    scipy.io.wavfile returns (uint8, int16, int32, int64, float32, float64)."""
     off = int(np.floor(u * (len(noise) - len(sig))))
     ns = noise[off:off + len(sig)]
     Es = np.mean(sig ** 2)

@@ -9,12 +9,12 @@ if [ -n "${PYTEST:-}" ]; then
   tail -1 $O/pytest.log
 fi
 : > $O/ab.txt
-for round in 1 2; do
+for round in $(seq ${ROUNDS:-2}); do
   for lib in "$LIB_A" "$LIB_B"; do
     FDLP_LIB=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-transfers ${BENCH_EXTRA:-} > $O/ab_run.log 2>&1 || { tail -20 $O/ab_run.log; exit 2; }
     python3 -c "
 import json,sys; d=json.loads(open('$O/ab_run.log').read().strip().splitlines()[-1])
-print(sys.argv[1].split('/')[-1], round(d['value'],1), 'one', round(d['one_batch_in_flight']['value'],1), {k: round(v,3) for k,v in d['stage_ms_per_step'].items()})" "$lib" >> $O/ab.txt
+print(sys.argv[1].split('/')[-1], round(d['value'],1), 'one', round(d['one_batch_in_flight']['value'],1), {k.replace('fdlp::','').replace('_kernel',''): round(v,3) for k,v in d.get('kernel_ms_per_launch', d['stage_ms_per_step']).items()})" "$lib" >> $O/ab.txt
   done
 done
 cat $O/ab.txt

@@ -155,6 +155,8 @@ SIGNATURES = {
     "fdlp_nprandom_rand": (c_i32, [c_p, c_i64, P_dbl]),
     "fdlp_nprandom_destroy": (c_i32, [c_p]),
     "fdlp_noise_params": (c_i32, [P_i16, c_i64, P_i16, c_i64, c_dbl, c_dbl, P_i64, P_dbl]),
+    "fdlp_noise_params_any": (c_i32, [P_dbl, c_i64, c_i32, P_i16, c_i64, c_dbl, c_dbl, P_i64, P_dbl]),
+    "fdlp_wav_kind": (c_i32, [P_u8, c_i64, P_i32]),
     "fdlp_wav_parse": (c_i32, [P_u8, c_i64, P_i32, P_i32, ctypes.POINTER(P_i16), P_i64]),
     "fdlp_wav_decode": (c_i32, [P_u8, c_i64, P_i32, P_i32, P_i32, P_i64, P_dbl]),
     "fdlp_job_run": (c_i32, [ctypes.POINTER(FdlpConfigC), c_i32, ctypes.c_char_p, ctypes.c_char_p,

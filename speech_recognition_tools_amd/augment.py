@@ -1,7 +1,8 @@
 """Host-side parameters of the reference's augmentations (the mixing itself runs on the device).
 
 add_noise_to_wav (features.py:24-31): offset = floor(rand()*(len(noise)-len(sig))),
-alpha = sqrt(E_s / (E_n * 10**(snr/10))) with E = mean(x**2) over int16-wrapped squares.
+alpha = sqrt(E_s / (E_n * 10**(snr/10))) with E = mean(x**2) over the squares in the signal's own dtype
+(int16 / int32 / uint8 squares wrap, float32 squares round and sum in float32; fdlp_noise_params_any).
 """
 import ctypes
 
@@ -12,9 +13,28 @@ from ._lib import check, lib, ptr
 DIFF_KERNEL = (1, 2, 3, 2, 0, -2, -5, -2, 0, 2, 3, 2, 1)  # computeFDLPSpectrogram.py:163
 
 
-def noise_params(sig: np.ndarray, noise: np.ndarray, snr: float, u: float):
-    s = np.ascontiguousarray(sig, dtype=np.int16)
+# scipy.io.wavfile dtypes -> include/fdlp.h FDLP_SIG_*
+SIG_KINDS = {"uint8": 1, "int16": 2, "int32": 3, "int64": 4, "float32": 5, "float64": 6}
+
+
+def noise_params(sig: np.ndarray, noise: np.ndarray, snr: float, u: float, kind: str = None):
+    """(offset, alpha) of add_noise_to_wav for the uniform draw u.  `kind` is scipy's dtype of the signal
+    (default: sig's own dtype; a float64 array read from a non-16-bit WAV carries it as `scipy_kind`,
+    featgen/features.read_wav_bytes)."""
+    kind = kind or getattr(sig, "scipy_kind", None) or str(np.asarray(sig).dtype)
+    if noise.dtype != np.int16:
+        raise NotImplementedError("noise files other than 16-bit PCM (the recipes' noises/*.wav are 16-bit)")
     n = np.ascontiguousarray(noise, dtype=np.int16)
+    if kind != "int16":
+        if kind not in SIG_KINDS:
+            raise ValueError("unsupported signal dtype %s" % kind)
+        s = np.ascontiguousarray(np.asarray(sig), dtype=np.float64)
+        off = ctypes.c_int64()
+        alpha = ctypes.c_double()
+        check(lib.fdlp_noise_params_any(ptr(s, ctypes.c_double), s.size, SIG_KINDS[kind], ptr(n, ctypes.c_int16),
+                                        n.size, float(snr), float(u), ctypes.byref(off), ctypes.byref(alpha)))
+        return off.value, alpha.value
+    s = np.ascontiguousarray(sig, dtype=np.int16)
     off = ctypes.c_int64()
     alpha = ctypes.c_double()
     check(lib.fdlp_noise_params(ptr(s, ctypes.c_int16), s.size, ptr(n, ctypes.c_int16), n.size, float(snr),

@@ -462,41 +462,12 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
 
   // straddles: A = x[m], m in [lb, b) (the region just below boundary b, at most nlags-1 long),
   // B = x[(m + l) mod N] for m + l >= b, x = W_j D
-  double* xa = xs;
-  double* xb = xs + kWin;
-#pragma unroll 1
-  for (int e = 0; e < (kw != 0.0 ? 2 : 3); ++e) {
-    const int b = e == 0 ? m1 : (e == 1 ? m2 : N);
-    int lb = e == 0 ? 0 : (e == 1 ? m1 : m2);
-    lb = max(lb, b - (nlags - 1));
-    if (lb >= b) continue;
-    constexpr int kSt = (kWin + 16 * NT + 63) / 64;  // B reads reach xb[kWin - 1 + 16 NT - 1]
-    double wv[kSt], dv[kSt];
-#pragma unroll
-    for (int u = 0; u < kSt; ++u) {  // all loads first: one exposed latency per boundary
-      const int pos = b - kWin + 64 * u + lane;
-      const int pm = pos < 0 ? 0 : (pos >= N ? pos - N : pos);
-      FDLP_CHECK(pm >= 0 && pm < N);
-      wv[u] = wrow[pm];
-      dv[u] = drow[pm];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kSt; ++u) {
-      const int q = 64 * u + lane;
-      const int pos = b - kWin + q;
-      const double x = pos >= lb ? wv[u] * dv[u] : 0.0;
-      if constexpr (VS) {
-        if (q < kWin + 16 * NT) xb[q] = pos >= b ? (e == 1 && pos < N ? (wv[u] - 1.0) * dv[u] : x) : 0.0;
-      } else {
-        if (q < kWin + 16 * NT) xb[q] = pos >= b ? x : 0.0;
-      }
-      if (q < kWin) xa[q] = pos < b ? x : 0.0;
-    }
-    __syncthreads();
+  constexpr int kSt = (kWin + 16 * NT + 63) / 64;  // B reads reach xb[kWin - 1 + 16 NT - 1]
+  static_assert(kSt > kWin / 64 && kWin % 64 == 0, "window layout");
+  // the MFMAs of one straddle from its staged windows xa / xb (B reads xb[kWin - 63, kWin + 16 NT))
+  auto straddle = [&](const double* xa, const double* xb, int st0) {
     // st unrolled, so each step's first live tile tmin is a constant: its MFMAs and their LDS reads are
     // branch-free (the reads issue together instead of one exposed LDS latency per MFMA)
-    const int st0 = (lb - b + kWin) >> 6;
 #pragma unroll
     for (int st = 0; st < kWin / 64; ++st) {
       if (st < st0) continue;
@@ -511,6 +482,97 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
 #pragma unroll
       for (int t = 0; t < NT; ++t)
         if (t >= tmin) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv[t], acc[t], 0, 0, 0);
+    }
+  };
+  // Regular band (72 of the recipes' 80): both straddle windows [b - kWin, b + kSt 64 - kWin) lie inside
+  // [0, N), the flat top is at least nlags - 1 wide (so the m1 straddle's B side is flat: x = D, and the m2
+  // straddle's A side is flat: x = D) and the wrap straddle is the shared kw Wrap.  Then nothing is masked
+  // or clamped: A positions below lb = b - (nlags - 1) pair only at lags >= nlags (their accumulator
+  // elements are never emitted), B below b reads a zeroed 64-position block, and the staging is a product (or
+  // a copy) per position with immediate-offset loads -- the same values the general staging writes at every
+  // position an emitted lag reads, so r is bit-identical.  The loads of both boundaries are issued at once
+  // into two compact LDS regions [A: kWin | zeros: 64 | B: 16 NT], so an item waits for memory once before
+  // its straddles instead of once per boundary.
+  constexpr int kReg = kWin + 64 + 16 * NT;  // one boundary's compact region
+  constexpr bool kFits = 2 * kReg <= kLds;   // every order up to p = 190 (NT <= 12)
+#ifdef FDLP_AB_BAND_GENERIC  // A/B build: every band through the general staging
+  const bool fast = false;
+#else
+  const bool fast = kFits && VS && kw != 0.0 && m1 >= kWin && m2 - m1 >= nlags - 1 && m2 + (kSt * 64 - kWin) <= N;
+#endif
+  if constexpr (kFits) if (fast) {
+    constexpr int kA = kWin / 64, kB = kSt - kWin / 64;  // staged A / B slots
+    static_assert(kB <= kA + 1, "m2 B taps");
+    double d1[kSt], w1[kA], d2[kSt], w2[kA];
+    {
+      const double* s1 = drow + (m1 - kWin) + lane;
+      const double* t1 = wrow + (m1 - kWin) + lane;        // taps below m1
+      const double* s2 = drow + (m2 - kWin) + lane;
+      const double* t2 = wrow + m2 + lane;                 // taps from m2 on
+      FDLP_CHECK(m1 - kWin >= 0 && m2 + 64 * kB <= N);
+#pragma unroll
+      for (int u = 0; u < kSt; ++u) d1[u] = s1[64 * u];
+#pragma unroll
+      for (int u = 0; u < kA; ++u) w1[u] = t1[64 * u];
+#pragma unroll
+      for (int u = 0; u < kSt; ++u) d2[u] = s2[64 * u];
+#pragma unroll
+      for (int u = 0; u < kA; ++u) w2[u] = t2[64 * u];
+    }
+    double* r1 = xs;
+    double* r2 = xs + kReg;
+#pragma unroll
+    for (int u = 0; u < kA; ++u) {
+      r1[64 * u + lane] = w1[u] * d1[u];  // lower-skirt taps x D below m1
+      r2[64 * u + lane] = d2[u];          // flat top below m2
+    }
+    r1[kWin + lane] = 0.0;
+    r2[kWin + lane] = 0.0;
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int q = 64 * u + lane;
+      if (q < 16 * NT) {
+        r1[kWin + 64 + q] = d1[kA + u];                                  // flat top from m1 on
+        r2[kWin + 64 + q] = u < kA ? (w2[u] - 1.0) * d2[kA + u] : 0.0;  // (W - 1) D from m2 on
+      }
+    }
+    __syncthreads();
+    straddle(r1, r1 + 64, 0);  // xb index k -> region offset k + 64: xb[kWin - 64 + i] is the zero block
+    straddle(r2, r2 + 64, 0);
+  }
+  if (!fast) {
+    double* xa = xs;
+    double* xb = xs + kWin;
+#pragma unroll 1
+    for (int e = 0; e < (kw != 0.0 ? 2 : 3); ++e) {
+      const int b = e == 0 ? m1 : (e == 1 ? m2 : N);
+      int lb = e == 0 ? 0 : (e == 1 ? m1 : m2);
+      lb = max(lb, b - (nlags - 1));
+      if (lb >= b) continue;
+      double wv[kSt], dv[kSt];
+#pragma unroll
+      for (int u = 0; u < kSt; ++u) {  // all loads first: one exposed latency per boundary
+        const int pos = b - kWin + 64 * u + lane;
+        const int pm = pos < 0 ? 0 : (pos >= N ? pos - N : pos);
+        FDLP_CHECK(pm >= 0 && pm < N);
+        wv[u] = wrow[pm];
+        dv[u] = drow[pm];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kSt; ++u) {
+        const int q = 64 * u + lane;
+        const int pos = b - kWin + q;
+        const double x = pos >= lb ? wv[u] * dv[u] : 0.0;
+        if constexpr (VS) {
+          if (q < kWin + 16 * NT) xb[q] = pos >= b ? (e == 1 && pos < N ? (wv[u] - 1.0) * dv[u] : x) : 0.0;
+        } else {
+          if (q < kWin + 16 * NT) xb[q] = pos >= b ? x : 0.0;
+        }
+        if (q < kWin) xa[q] = pos < b ? x : 0.0;
+      }
+      __syncthreads();
+      straddle(xa, xb, (lb - b + kWin) >> 6);
     }
   }
   __syncthreads();

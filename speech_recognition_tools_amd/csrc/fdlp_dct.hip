@@ -39,8 +39,11 @@ __device__ __forceinline__ double makhoul_sample(const DevConsts& c, const Frame
       s = __dadd_rn(s, __dmul_rn(fd.alpha, ns));
     }
   } else if (pcm_kind == 1) {
+    // the double values of scipy's array for the other WAV formats (uint8 / int32 / int64 / float32 /
+    // float64); noise mixing as for int16: sig + alp*ns in fp64 (features.py:31, any dtype + float64)
     s = ((const double*)pcm)[fd.pcm_off + t];
-  } else {
+    if (fd.noise_off >= 0) s = __dadd_rn(s, __dmul_rn(fd.alpha, (double)noise[fd.noise_off + t]));
+  } else if (pcm_kind == 2) {
     // pcm_kind 2: scipy.signal.convolve(int16 s, diff kernel, 'same') -> int64, exact
     // (computeFDLPSpectrogram.py:162-164); 'same' = full[6 : 6+T], zeros outside [0, T)
     const int16_t* x = (const int16_t*)pcm + fd.pcm_off;
@@ -51,6 +54,18 @@ __device__ __forceinline__ double makhoul_sample(const DevConsts& c, const Frame
       if (idx >= 0 && idx < fd.T) acc += (long long)kDiffTaps[q] * (long long)x[idx];
     }
     s = (double)acc;
+  } else {
+    // pcm_kind 3: the same 'same' convolution of a non-int16 signal (its double values): scipy takes the
+    // direct route (np.convolve, float64 or int64 sums), here a float64 dot in increasing sample order; the
+    // products tap x sample are exact and so are the sums of any integer or 16/24-bit-scaled signal
+    const double* x = (const double*)pcm + fd.pcm_off;
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 12; q >= 0; --q) {
+      const int64_t idx = t + 6 - q;
+      if (idx >= 0 && idx < fd.T) acc = __dadd_rn(acc, __dmul_rn((double)kDiffTaps[q], x[idx]));
+    }
+    s = acc;
   }
   return __dmul_rn(s, c.hamming[m]);  // frame * win (features.py:153)
 }

@@ -159,6 +159,92 @@ int fdlp_noise_params(const int16_t* sig, int64_t T, const int16_t* noise, int64
   return FDLP_OK;
 }
 
+}  // extern "C"
+
+// numpy's float reduction as np.mean runs it (numpy/_core/src/umath/loops_utils.h.src pairwise_sum): the
+// array is fed to the add loop in 8192-element chunks (the iterator's buffer), each chunk summed pairwise
+// (8 accumulators up to 128 elements, halves above, the halves cut at a multiple of 8) and added to the
+// running result, which starts at 0.  Acc is the reduction dtype (float for float32 input, double otherwise);
+// pinned against np.mean in tests/test_noise_kinds.py.
+template <typename Acc>
+static Acc np_pairwise(const Acc* a, int64_t n) {
+  if (n < 8) {
+    Acc res = 0;
+    for (int64_t i = 0; i < n; ++i) res = res + a[i];
+    return res;
+  }
+  if (n <= 128) {
+    Acc r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int64_t i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] = r[j] + a[i + j];
+    Acc res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res = res + a[i];
+    return res;
+  }
+  int64_t n2 = n / 2;
+  n2 -= n2 % 8;
+  return np_pairwise(a, n2) + np_pairwise(a + n2, n - n2);
+}
+
+// np.mean(sig ** 2) with sig in scipy's dtype `kind` (its values given as doubles): the square in that dtype
+// (integers wrap, float32 rounds), then the chunked pairwise sum of np_pairwise in the reduction dtype
+static double np_mean_square(const double* sig, int64_t T, int kind) {
+  constexpr int64_t kChunk = 8192;
+  if (kind == FDLP_SIG_F32) {
+    std::vector<float> sq((size_t)std::min(T, kChunk));
+    float res = 0.0f;
+    for (int64_t c0 = 0; c0 < T; c0 += kChunk) {
+      const int64_t n = std::min(kChunk, T - c0);
+      for (int64_t i = 0; i < n; ++i) {
+        const float x = (float)sig[c0 + i];
+        sq[(size_t)i] = x * x;
+      }
+      res = res + np_pairwise(sq.data(), n);
+    }
+    return (double)(res / (float)T);  // np.float32 scalar / int count: a float32 division (NEP 50)
+  }
+  std::vector<double> sq((size_t)std::min(T, kChunk));
+  double res = 0.0;
+  for (int64_t c0 = 0; c0 < T; c0 += kChunk) {
+    const int64_t n = std::min(kChunk, T - c0);
+    for (int64_t i = 0; i < n; ++i) {
+      const double v = sig[c0 + i];
+      double q;
+      switch (kind) {
+        case FDLP_SIG_U8: { const uint8_t x = (uint8_t)(int)v; q = (double)(uint8_t)(x * x); break; }
+        case FDLP_SIG_I16: { const int16_t x = (int16_t)v; q = (double)(int16_t)(uint16_t)((uint32_t)(int32_t)x * (uint32_t)(int32_t)x); break; }
+        case FDLP_SIG_I32: { const int32_t x = (int32_t)v; q = (double)(int32_t)((uint32_t)x * (uint32_t)x); break; }
+        case FDLP_SIG_I64: { const int64_t x = (int64_t)v; q = (double)(int64_t)((uint64_t)x * (uint64_t)x); break; }
+        default: q = v * v; break;  // float64
+      }
+      sq[(size_t)i] = q;
+    }
+    res = res + np_pairwise(sq.data(), n);
+  }
+  return res / (double)T;
+}
+
+extern "C" {
+
+int fdlp_noise_params_any(const double* sig, int64_t T, int32_t kind, const int16_t* noise, int64_t noise_len,
+                          double snr, double u, int64_t* off, double* alpha) {
+  if (!sig || !noise || !off || !alpha || T <= 0 || kind < FDLP_SIG_U8 || kind > FDLP_SIG_F64)
+    return fdlp::fail(FDLP_E_INVALID, "fdlp_noise_params_any: bad args");
+  const double span = (double)(noise_len - T);  // features.py:25
+  const int64_t o = (int64_t)floor(u * span);
+  if (o < 0 || o + T > noise_len)
+    return fdlp::fail(FDLP_E_INVALID, "noise file shorter than the utterance (reference slices a short noise)");
+  int64_t en = 0;  // the int16 noise's wrapped squares, exactly (features.py:28)
+  for (int64_t t = 0; t < T; ++t)
+    en += (int16_t)(uint16_t)((uint32_t)(int32_t)noise[o + t] * (uint32_t)(int32_t)noise[o + t]);
+  const double Es = np_mean_square(sig, T, kind), En = (double)en / (double)T;
+  *alpha = sqrt(Es / (En * pow(10.0, snr / 10.0)));  // (features.py:29)
+  *off = o;
+  return FDLP_OK;
+}
+
 // Compact ark codes -> the float32 ark values (fdlp_batch.out_q_dev, fdlp_device.h q_code): the device
 // stores (float)(k / 10^d) in out_dev; here the same two IEEE operations on the same k, so the floats
 // are bitwise the ones the device would have written.  -32768 is -0.0.  The 65536 values of a decimals
@@ -333,6 +419,22 @@ int fdlp_wav_decode(const uint8_t* buf, int64_t len, int32_t* srate, int32_t* ch
   if (out) {
     const int64_t n = w.frames * w.ch;
     for (int64_t i = 0; i < n; ++i) out[i] = wav_sample(w, i);
+  }
+  return FDLP_OK;
+}
+
+int fdlp_wav_kind(const uint8_t* buf, int64_t len, int32_t* kind) {
+  if (!kind) return fdlp::fail(FDLP_E_INVALID, "fdlp_wav_kind: bad args");
+  WavInfo w;
+  int rc = wav_info(buf, len, &w);
+  if (rc != FDLP_OK) return rc;
+  if (w.fmt == 3) {
+    *kind = w.bps == 4 ? FDLP_SIG_F32 : FDLP_SIG_F64;
+  } else if (w.bits <= 8) {
+    *kind = FDLP_SIG_U8;
+  } else {
+    const int cont = (w.bps == 1 || w.bps == 2 || w.bps == 4 || w.bps == 8) ? w.bps : (w.bps == 3 ? 4 : 8);
+    *kind = cont == 2 ? FDLP_SIG_I16 : (cont == 4 ? FDLP_SIG_I32 : FDLP_SIG_I64);
   }
   return FDLP_OK;
 }

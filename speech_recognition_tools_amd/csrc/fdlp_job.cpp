@@ -54,6 +54,7 @@ struct Utt {
   std::shared_ptr<std::vector<uint8_t>> raw;   // the file bytes; is_int16: the samples point into them
   const int16_t* s16 = nullptr;
   std::shared_ptr<std::vector<double>> f64;    // otherwise (scipy's dtype, converted exactly as numpy does)
+  int32_t kind = FDLP_SIG_I16;                  // scipy's dtype of the samples (fdlp_wav_kind)
 };
 
 // memcpy jobs (utterance samples -> the pinned batch buffer) on a few threads; a job keeps its source
@@ -240,7 +241,8 @@ void read_entry(const std::string& line, Utt& u) {
   } else {
     u.f64 = std::make_shared<std::vector<double>>((size_t)n * ch);
     if (fdlp_wav_decode(bytes->data(), (int64_t)bytes->size(), nullptr, nullptr, nullptr, nullptr, u.f64->data()) !=
-        FDLP_OK)
+            FDLP_OK ||
+        fdlp_wav_kind(bytes->data(), (int64_t)bytes->size(), &u.kind) != FDLP_OK)
       return;
   }
   u.ok = true;
@@ -1263,14 +1265,13 @@ extern "C" int fdlp_job_run(const fdlp_config* cfg, int device, const char* scp_
     fdlp_geometry(plan, T, &F, &L);
     if (F < 1) return cleanup(fail(FDLP_E_INVALID, "invalid number of data points (0) specified"));
     const int kind = u.is_int16 ? FDLP_PCM_I16 : FDLP_PCM_F64;
-    if ((o->noise || o->preprocess == FDLP_PRE_DIFF) && kind != FDLP_PCM_I16)
-      return cleanup(fail(FDLP_E_INVALID, "noise mixing / diff preprocessing need 16-bit PCM input"));
     int64_t noff = 0;
     double alpha = 0.0;
     if (o->noise) {  // add_noise_to_wav (features.py:24-31), np.random.rand() per utterance (:166)
       double uu = 0.0;
       JOB_TRY(fdlp_nprandom_rand(nrng, 1, &uu));
-      JOB_TRY(fdlp_noise_params(u.s16, T, o->noise, o->noise_len, o->snr, uu, &noff, &alpha));
+      if (kind == FDLP_PCM_I16) JOB_TRY(fdlp_noise_params(u.s16, T, o->noise, o->noise_len, o->snr, uu, &noff, &alpha));
+      else JOB_TRY(fdlp_noise_params_any(u.f64->data(), T, u.kind, o->noise, o->noise_len, o->snr, uu, &noff, &alpha));
     }
     if (o->progress_name) printf("%s: Computing Features for file: %s\n", o->progress_name, u.id.c_str());  // :185
     // a batch is one PCM kind and at most max_frames frames

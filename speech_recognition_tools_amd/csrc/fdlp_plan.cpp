@@ -958,11 +958,11 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
   if (b->n_utt < 0 || (b->n_utt > 0 && (!b->pcm_dev || !b->pcm_off || !b->utt_len || !b->out_row)))
     return fail(FDLP_E_INVALID, "fdlp_compute: missing batch arrays");
   if (b->pcm_kind != FDLP_PCM_I16 && b->pcm_kind != FDLP_PCM_F64) return fail(FDLP_E_INVALID, "bad pcm_kind");
-  if (b->noise_dev && (b->pcm_kind != FDLP_PCM_I16 || !b->noise_off || !b->noise_alpha))
-    return fail(FDLP_E_INVALID, "noise mixing needs int16 PCM, noise_off and noise_alpha");
+  if (b->noise_dev && (!b->noise_off || !b->noise_alpha))
+    return fail(FDLP_E_INVALID, "noise mixing needs noise_off and noise_alpha");
   if (b->preprocess != FDLP_PRE_NONE && b->preprocess != FDLP_PRE_DIFF) return fail(FDLP_E_INVALID, "bad preprocess");
-  if (b->preprocess == FDLP_PRE_DIFF && (b->pcm_kind != FDLP_PCM_I16 || b->noise_dev))
-    return fail(FDLP_E_INVALID, "diff preprocessing needs int16 PCM and no noise mixing");
+  if (b->preprocess == FDLP_PRE_DIFF && b->noise_dev)
+    return fail(FDLP_E_INVALID, "diff preprocessing and noise mixing are exclusive (computeFDLPSpectrogram.py:160-166)");
   if (!b->out_dev && !b->out_f64_dev && !b->out_q_dev) return fail(FDLP_E_INVALID, "fdlp_compute: no output buffer");
   if (b->out_q_dev && (b->ark_decimals < 0 || !b->out_q_flag_dev || p->modspec))
     return fail(FDLP_E_INVALID, "fdlp_compute: out_q_dev needs ark_decimals >= 0, out_q_flag_dev and a spectrogram plan");
@@ -1062,7 +1062,8 @@ int fdlp_compute(fdlp_plan* p, const fdlp_batch* b, void* stream) {
     double* gg_dbg = p->debug_intermediates ? p->ws.gg + it0 : nullptr;
     double* cep_dbg = (p->debug_intermediates || p->modspec) ? p->ws.cep + it0 * p->M : nullptr;
     HIP_TRY(mark(0));
-    const int pcm_kind = b->preprocess == FDLP_PRE_DIFF ? 2 : b->pcm_kind;
+    // the sample gather's kinds: 0 int16, 1 float64 values of another WAV dtype, 2 / 3 the diff filter on them
+    const int pcm_kind = b->preprocess == FDLP_PRE_DIFF ? (b->pcm_kind == FDLP_PCM_I16 ? 2 : 3) : b->pcm_kind;
     if (dct_fused(p)) {  // one kernel per frame; the second DCT stage mark follows it directly
       HIP_TRY(fdlp::launch_dct_frame(p->dc, b->pcm_dev, pcm_kind, b->noise_dev, p->d_frames + f0, nullptr, n,
                                      p->ws.dct + f0 * N, st));

@@ -160,8 +160,6 @@ def getFeats(args, srate=16000, window=np.hamming, return_feats=True):
                 continue
             if sig.ndim != 1:
                 raise ValueError("multi-channel WAV input is not supported (the reference expects mono)")
-            if sig.dtype != np.int16 and (noise is not None or diff):
-                raise NotImplementedError("noise mixing / diff preprocessing need 16-bit PCM input")
             if pending and pending[-1][1].dtype != sig.dtype:
                 flush()  # a device batch holds one sample type (int16 or the float64 of other formats)
             T = sig.shape[0]

@@ -19,6 +19,19 @@ import numpy as np
 from .._lib import FdlpConfigC, FDLP_FBANK_COCHLEAR, FDLP_FBANK_MEL, check, lib, ptr
 
 
+class WavSamples(np.ndarray):
+    """float64 samples of a non-16-bit WAV with scipy's dtype kept as `scipy_kind` ('uint8', 'int32',
+    'int64', 'float32', 'float64'): the reference squares the signal in that dtype when it mixes noise
+    (features.py:27), so augment.noise_params needs it."""
+    scipy_kind = None
+
+    def __array_finalize__(self, obj):
+        self.scipy_kind = getattr(obj, "scipy_kind", None)
+
+
+_KIND_NAMES = {1: "uint8", 2: "int16", 3: "int32", 4: "int64", 5: "float32", 6: "float64"}
+
+
 def read_wav_bytes(data: bytes):
     """(sr, samples) of a RIFF/WAVE buffer like scipy.io.wavfile.read (computeFDLPSpectrogram.py:133,:139):
     int16 for 16-bit PCM; the other formats scipy reads (8-bit unsigned, 24/32/64-bit integer, float32/64)
@@ -44,6 +57,10 @@ def read_wav_bytes(data: bytes):
         x = np.empty(n.value * ch.value, dtype=np.float64)
         check(lib.fdlp_wav_decode(ptr(buf, ctypes.c_uint8), buf.size, None, None, None, None,
                                   ptr(x, ctypes.c_double)))
+        kind = ctypes.c_int32()
+        check(lib.fdlp_wav_kind(ptr(buf, ctypes.c_uint8), buf.size, ctypes.byref(kind)))
+        x = x.view(WavSamples)
+        x.scipy_kind = _KIND_NAMES[kind.value]
     if ch.value > 1:
         x = x.reshape(-1, ch.value)
     return sr.value, x

@@ -25,7 +25,7 @@ def load_golden(name):
 
 
 GOLDEN_SETS = ["wsj", "reverb", "chime4_noise", "cli_default_mel", "mel80", "wsj_diff", "gamma_lifter_odd",
-               "reverb_rir", "reverb_rir_noise"]
+               "reverb_rir", "reverb_rir_noise", "wav_kinds_noise", "wav_kinds_diff"]
 
 
 def oracle_cfg(meta):

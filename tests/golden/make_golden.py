@@ -73,8 +73,22 @@ def synthetic_rir(R, seed, t60=0.25):
     return np.clip(np.round(h * 32767), -32768, 32767).astype(np.int16)
 
 
-def run_reference(signals, opts, seed, noise_seed=None, noise=None, noise_name=None, rir=None):
-    """Write WAVs + scp, call getFeats with an argparse Namespace, capture the dict."""
+def wav24_bytes(v, sr=16000):
+    """A mono 24-bit PCM RIFF file of the int32 values v (|v| < 2**23): scipy.io.wavfile.write has no 24-bit
+    writer; scipy reads it back as int32 v << 8 (left-justified)."""
+    import struct
+    v = np.asarray(v, dtype=np.int64)
+    data = bytearray()
+    for x in v:
+        data += int(x & 0xFFFFFF).to_bytes(3, "little")
+    fmt = struct.pack("<HHIIHH", 1, 1, sr, sr * 3, 3, 24)
+    body = b"WAVE" + b"fmt " + struct.pack("<I", len(fmt)) + fmt + b"data" + struct.pack("<I", len(data)) + bytes(data)
+    return b"RIFF" + struct.pack("<I", len(body)) + body
+
+
+def run_reference(signals, opts, seed, noise_seed=None, noise=None, noise_name=None, rir=None, raw=None):
+    """Write WAVs + scp, call getFeats with an argparse Namespace, capture the dict.  raw: {utt: file bytes}
+    written as they are instead of wavfile.write(signals[utt])."""
     sys.path.insert(0, os.path.join(REF, "src/featgen"))
     import computeFDLPSpectrogram as cf  # noqa: E402
 
@@ -89,7 +103,11 @@ def run_reference(signals, opts, seed, noise_seed=None, noise=None, noise_name=N
         with open(scp, "w") as f:
             for utt, x in signals.items():
                 p = os.path.join(td, utt + ".wav")
-                wavfile.write(p, 16000, x)
+                if raw and utt in raw:
+                    with open(p, "wb") as fw:
+                        fw.write(raw[utt])
+                else:
+                    wavfile.write(p, 16000, x)
                 f.write("%s %s\n" % (utt, p))
         cwd = os.getcwd()
         if noise is not None:
@@ -385,9 +403,56 @@ def reverb_rir_fixture():
          extra=dict(noise_seed=4), more={"rir": rir, "noise_babble": noise})
 
 
+def wav_kinds_fixtures():
+    """Noise mixing (--add_noise babble,20) and the diff filter (--add_noise diff) on the WAV formats scipy
+    reads as other dtypes than int16 (features.py:24-31 squares the signal in its own dtype; :162-164 convolves
+    it): float32 (a 16-bit-scaled signal and an unscaled one), 24-bit PCM (int32, left-justified), 32-bit PCM
+    (int32, squares that wrap) and 8-bit unsigned PCM.  The WAV bytes are stored (wav_<utt>) with scipy's
+    array (in_<utt>) and the reference's features (out_<utt>)."""
+    import io
+    sig, raw = OrderedDict(), {}
+    sig["f32"] = (speech_like(24000, 61).astype(np.float64) / 32768.0).astype(np.float32)
+    sig["f32big"] = (speech_like(20000, 62).astype(np.float64) * 0.37).astype(np.float32)
+    # 24/32-bit squares wrap in int32, so the reference's mean energy can come out negative (alpha NaN, and
+    # solve_toeplitz raises): the first seeds whose wrapped mean is positive are used
+    seed = 63
+    while True:
+        v24 = np.clip(speech_like(40000, seed).astype(np.int64) * 211, -(2 ** 23), 2 ** 23 - 1)
+        if np.mean((v24 << 8).astype(np.int32) ** 2) > 0:
+            break
+        seed += 100
+    raw["i24"] = wav24_bytes(v24)
+    sig["i24"] = wavfile.read(io.BytesIO(raw["i24"]))[1]
+    assert sig["i24"].dtype == np.int32 and np.array_equal(sig["i24"], (v24 << 8).astype(np.int32))
+    seed = 64
+    while True:
+        sig["i32"] = (speech_like(30000, seed).astype(np.int64) * 12).astype(np.int32)
+        if np.mean(sig["i32"] ** 2) > 0:
+            break
+        seed += 100
+    sig["u8"] = np.clip(speech_like(17000, 65).astype(np.int64) // 64 + 128, 0, 255).astype(np.uint8)
+    for u, x in sig.items():
+        if u not in raw:
+            b = io.BytesIO()
+            wavfile.write(b, 16000, x)
+            raw[u] = b.getvalue()
+        assert wavfile.read(io.BytesIO(raw[u]))[1].dtype == x.dtype
+    more = {"wav_" + u: np.frombuffer(raw[u], dtype=np.uint8) for u in sig}
+    noise = white(16000 * 5, 66, scale=1200.0)
+    opts = dict(CHIME4, add_noise="babble,20")
+    save("wav_kinds_noise", sig, opts, 77,
+         run_reference(sig, opts, 77, noise_seed=5, noise=noise, noise_name="babble", raw=raw),
+         extra=dict(noise_seed=5), more=dict(more, noise_babble=noise))
+    opts = dict(WSJ, add_noise="diff")
+    save("wav_kinds_diff", sig, opts, 78, run_reference(sig, opts, 78, raw=raw), more=more)
+
+
 def main():
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
     sys.dont_write_bytecode = True
+    if "--wav-kinds-only" in sys.argv:
+        wav_kinds_fixtures()
+        return
     if "--reverb-only" in sys.argv:
         reverb_rir_fixture()
         return

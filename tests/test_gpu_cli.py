@@ -366,3 +366,29 @@ def test_cli_add_reverb(tmp_path, monkeypatch, name):
     out = str(d / "rv")
     getFeats(_args([scp, out] + _opts(meta) + extra))
     _check(out, meta, ref, meta["utts"])
+
+
+@RUNNERS
+@pytest.mark.parametrize("name", ["wav_kinds_noise", "wav_kinds_diff"])
+def test_cli_noise_and_diff_on_other_wav_formats(tmp_path, monkeypatch, runner, name):
+    """--add_noise babble,20 and --add_noise diff on float32, 24-bit, 32-bit and 8-bit WAVs
+    (the reference mixes / convolves whatever dtype scipy.io.wavfile.read returns, features.py:24-31,
+    computeFDLPSpectrogram.py:160-166), the WAV files themselves as the reference read them, against the
+    reference's features (tests/golden/make_golden.py wav_kinds_fixtures)."""
+    meta, sig, ref, z = load_golden(name)
+    (tmp_path / "noises").mkdir()
+    if "noise_babble" in z.files:
+        wavfile.write(str(tmp_path / "noises" / "babble.wav"), 16000, z["noise_babble"])
+    scp = str(tmp_path / "wav.scp")
+    with open(scp, "w") as f:
+        for u in meta["utts"]:
+            p = tmp_path / (u + ".wav")
+            p.write_bytes(z["wav_" + u].tobytes())
+            f.write("%s %s\n" % (u, p))
+    monkeypatch.chdir(str(tmp_path))
+    out = str(tmp_path / "k")
+    extra = ["--add_noise=" + meta["opts"]["add_noise"]]
+    if "noise_seed" in meta["extra"]:
+        extra.append("--noise_seed=%d" % meta["extra"]["noise_seed"])
+    _run([scp, out] + _opts(meta) + extra, runner)
+    _check(out, meta, ref, meta["utts"])

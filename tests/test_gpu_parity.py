@@ -25,11 +25,12 @@ def _batch_inputs(meta, sig, z):
     utts = meta["utts"]
     an = meta["opts"].get("add_noise", "clean")
     kw = {}
+    # other WAV dtypes (wav_kinds_*) go to the device as their float64 values (FDLP_PCM_F64)
+    wide = any(sig[u].dtype != np.int16 for u in utts)
+    pcm = np.concatenate([sig[u].astype(np.float64) if wide else sig[u] for u in utts])
     if an == "diff":
-        pcm = np.concatenate([sig[u] for u in utts])
         kw = dict(preprocess="diff")
     else:
-        pcm = np.concatenate([sig[u] for u in utts])
         if an != "clean":
             noise = z["noise_babble"]
             snr = float(an.split(",")[1])
