@@ -345,7 +345,7 @@ enum { FDLP_SIG_U8 = 1, FDLP_SIG_I16 = 2, FDLP_SIG_I32 = 3, FDLP_SIG_I64 = 4, FD
 /* The same for a signal of any of those dtypes, given as the double values of scipy's array (ABI 9): the
  * reference squares the signal in its own dtype (integer squares wrap, float32 squares round to float32) and
  * np.mean sums them like numpy (8192-element chunks, pairwise inside a chunk; float32 accumulated in float32),
- * features.py:27.  The noise is int16 (noises/*.wav of the recipes). */
+ * features.py:27.  The noise is int16 (noises/<name>.wav of the recipes). */
 int fdlp_noise_params_any(const double* sig, int64_t T, int32_t sig_kind, const int16_t* noise,
                           int64_t noise_len, double snr, double u, int64_t* off, double* alpha);
 
