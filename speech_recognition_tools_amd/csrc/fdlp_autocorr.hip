@@ -592,20 +592,24 @@ __global__ __launch_bounds__(64, 4) void ac_band_kernel(DevConsts c, const doubl
     const int pmask = fb.y & ((1 << (c.fl_H - 1)) - 1);  // parts h < fl_H - 1 added in increasing h
     double rv[kNB], uv[kNB], fv[kNB], wv[kNB];
     const double* wo = rwrap + (int64_t)f * nlags;
+    // lag L = 32 g + lane / 2 from one lane pointer and immediate offsets: lags past the row end read the next
+    // row (or the kRowSlack doubles every row buffer carries past its last row) and are never emitted
+    static_assert(32 * kNB - (16 * (NT - 1) - 14) <= kRowSlack, "row slack covers the last lag block");
+    const int lh = lane >> 1;
+    FDLP_CHECK(32 * kNB <= nlags + kRowSlack);
 #pragma unroll
     for (int g = 0; g < kNB; ++g) {
-      const int L = min(32 * g + (lane >> 1), nlags - 1);  // clamped: the loads are unconditional
-      rv[g] = ro[L];
-      uv[g] = uo[L];
-      fv[g] = fo[L];
-      wv[g] = kw != 0.0 ? wo[L] : 0.0;
+      rv[g] = ro[lh + 32 * g];
+      uv[g] = uo[lh + 32 * g];
+      fv[g] = fo[lh + 32 * g];
+      wv[g] = kw != 0.0 ? wo[lh + 32 * g] : 0.0;
     }
     if (pmask) {
       for (int rest = pmask; rest; rest &= rest - 1) {
         FDLP_CHECK(__builtin_ctz(rest) < c.fl_H - 1 && fb.x >= 0 && fb.x < kMaxChains);
-        const double* po = rpart + (((int64_t)f * (c.fl_H - 1) + __builtin_ctz(rest)) * kMaxChains + fb.x) * nlags;
+        const double* po = rpart + (((int64_t)f * (c.fl_H - 1) + __builtin_ctz(rest)) * kMaxChains + fb.x) * nlags + lh;
 #pragma unroll
-        for (int g = 0; g < kNB; ++g) fv[g] += po[min(32 * g + (lane >> 1), nlags - 1)];
+        for (int g = 0; g < kNB; ++g) fv[g] += po[32 * g];
       }
     }
 #pragma unroll
@@ -793,26 +797,70 @@ __global__ __launch_bounds__(64, vs_waves_per_simd<C>()) void ac_vsweep_kernel(D
   double pf[kPf], pe[C == 0 ? kPf : 1];
   // unconditional (clamped) loads: no branches around them, and their registers are read only in
   // commit, one chunk later, so the wait for them is not pulled into the FMA loop
-  auto issue = [&](int base) {
+  // A skirt-sweep chunk that lies inside [0, N) (every chunk but the sweep's first and last) needs no clamping
+  // or range selects: one lane pointer and immediate offsets (the general form spends ~10 integer VALU
+  // instructions per load and per slot on the clamps, the reversed index and the mirror test).  Chunks start
+  // at multiples of kVsChunk, so their ring slots are one aligned run and only the run at slot 0 writes the
+  // mirror (slots < kVsMirror = its first 16 positions).  (The flat sweep, which holds its chains in
+  // registers, spills with the second copy: 0.90 -> 1.18 ms; it keeps the general form.)
+  static_assert((kVsRing & (kVsRing - 1)) == 0 && kVsRing % kVsChunk == 0 && kVsMirror == 16, "aligned chunk runs");
+  auto inside = [&](int base) { return C == 0 && base >= 0 && base + kVsChunk <= N; };
+  auto issue = [&](int base) __attribute__((always_inline)) {
+    if (inside(base)) {  // wave-uniform
+      if (kind == 0) {
+        const double* pd = drow + (N - 1 - base - l);
+        const double* pw = ew + (N - 1 - base - l);
 #pragma unroll
-    for (int q = 0; q < kPf; ++q) {
-      const int n = min(max(base + 16 * q + l, 0), N - 1);
-      const int m = kind == 0 ? N - 1 - n : n;
-      pf[q] = __builtin_nontemporal_load(drow + m);
-      if constexpr (C == 0) pe[q] = ew[m];
+        for (int q = 0; q < kPf; ++q) {
+          pf[q] = __builtin_nontemporal_load(pd - 16 * q);
+          if constexpr (C == 0) pe[q] = pw[-16 * q];
+        }
+      } else {
+        const double* pd = drow + base + l;
+        const double* pw = ew + base + l;
+#pragma unroll
+        for (int q = 0; q < kPf; ++q) {
+          pf[q] = __builtin_nontemporal_load(pd + 16 * q);
+          if constexpr (C == 0) pe[q] = pw[16 * q];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < kPf; ++q) {
+        const int n = min(max(base + 16 * q + l, 0), N - 1);
+        const int m = kind == 0 ? N - 1 - n : n;
+        pf[q] = __builtin_nontemporal_load(drow + m);
+        if constexpr (C == 0) pe[q] = ew[m];
+      }
     }
   };
-  auto commit = [&](int base) {
+  auto commit = [&](int base) __attribute__((always_inline)) {
+    if (inside(base)) {  // wave-uniform
+      const int sb = base & (kVsRing - 1);
+      double* w = rg + sb + l;
 #pragma unroll
-    for (int q = 0; q < kPf; ++q) {
-      const int n = base + 16 * q + l;
-      const int slot = slot_add(base, 16 * q + l);
-      double v = pf[q];
-      if constexpr (C == 0) v = pe[q] * v;
-      v = (n >= 0 && n < N) ? v : 0.0;
-      FDLP_CHECK(slot >= 0 && slot < kVsRing);
-      rg[slot] = v;
-      if (slot < kVsMirror) rg[kVsRing + slot] = v;
+      for (int q = 0; q < kPf; ++q) {
+        double v = pf[q];
+        if constexpr (C == 0) v = pe[q] * v;
+        w[16 * q] = v;
+      }
+      if (sb == 0) {
+        double v = pf[0];
+        if constexpr (C == 0) v = pe[0] * v;
+        rg[kVsRing + l] = v;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < kPf; ++q) {
+        const int n = base + 16 * q + l;
+        const int slot = slot_add(base, 16 * q + l);
+        double v = pf[q];
+        if constexpr (C == 0) v = pe[q] * v;
+        v = (n >= 0 && n < N) ? v : 0.0;
+        FDLP_CHECK(slot >= 0 && slot < kVsRing);
+        rg[slot] = v;
+        if (slot < kVsMirror) rg[kVsRing + slot] = v;
+      }
     }
   };
   const int b_top = (nhi - 1) / A;
@@ -871,7 +919,7 @@ __global__ __launch_bounds__(64, vs_waves_per_simd<C>()) void ac_vsweep_kernel(D
   // chunks [lo_loaded, lo_loaded + 512) resident; the top block needs up to A b_top + 17 A - 2
   int lo_loaded = ((A * b_top + 17 * A - 1 + kVsChunk - 1) / kVsChunk) * kVsChunk;
   issue(lo_loaded - kVsChunk);
-  auto ensure = [&](int n0) {
+  auto ensure = [&](int n0) __attribute__((always_inline)) {
     while (n0 < lo_loaded) {  // wave-uniform
       lo_loaded -= kVsChunk;
       commit(lo_loaded);

@@ -48,6 +48,9 @@ struct SkSnap {
 
 constexpr int kMaxFlatParts = 4;
 constexpr int kMaxChains = 8;
+// doubles every autocorrelation row buffer (r, r_up, r_flat, r_wrap, r_flat_part) carries past its last row:
+// ac_band_kernel reads its combine rows in whole 32-lag blocks (lags up to 32 ceil(nlags / 32) - 1)
+constexpr int kRowSlack = 64;
 
 // One event of the flat-top sweep (ac_vsweep_kernel): at sweep position S (after the positions >= S
 // are consumed) restart (type 0) or emit (type 1) chain `chain`, which serves band `band`.

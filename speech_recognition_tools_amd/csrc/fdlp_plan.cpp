@@ -853,16 +853,16 @@ int fdlp_plan_create(const fdlp_config* cfg, int device, fdlp_plan** out) {
   p->max_frames = c.max_frames;
   if ((!dct_fused(p) && hipMalloc((void**)&p->ws.z, sizeof(double2) * F * p->nfft_c) != hipSuccess) ||
       hipMalloc((void**)&p->ws.dct, sizeof(double) * F * N) != hipSuccess ||
-      hipMalloc((void**)&p->ws.r, sizeof(double) * items * p->nlags * (p->cplx ? 2 : 1)) != hipSuccess ||
+      hipMalloc((void**)&p->ws.r, sizeof(double) * (items * p->nlags * (p->cplx ? 2 : 1) + fdlp::kRowSlack)) != hipSuccess ||
       hipMalloc((void**)&p->ws.gg, sizeof(double) * items) != hipSuccess ||
       (d.lpc_split && hipMalloc((void**)&p->ws.a_pad, sizeof(double) * items * d.lpc_astride) != hipSuccess) ||
       (p->modspec && hipMalloc((void**)&p->ws.cep, sizeof(double) * items * M) != hipSuccess) ||
       hipMalloc((void**)&p->ws.env, sizeof(double) * items * p->kk) != hipSuccess ||
-      (p->sk_avail && hipMalloc((void**)&p->r_up, sizeof(double) * items * p->nlags) != hipSuccess) ||
-      (p->vs_avail && hipMalloc((void**)&p->r_flat, sizeof(double) * items * p->nlags) != hipSuccess) ||
-      (p->vs_avail && p->d_sk_wrap && hipMalloc((void**)&p->r_wrap, sizeof(double) * F * p->nlags) != hipSuccess) ||
+      (p->sk_avail && hipMalloc((void**)&p->r_up, sizeof(double) * (items * p->nlags + fdlp::kRowSlack)) != hipSuccess) ||
+      (p->vs_avail && hipMalloc((void**)&p->r_flat, sizeof(double) * (items * p->nlags + fdlp::kRowSlack)) != hipSuccess) ||
+      (p->vs_avail && p->d_sk_wrap && hipMalloc((void**)&p->r_wrap, sizeof(double) * (F * p->nlags + fdlp::kRowSlack)) != hipSuccess) ||
       (p->vs_avail && p->sk.fl_H > 1 &&
-       hipMalloc((void**)&p->r_flat_part, sizeof(double) * F * (p->sk.fl_H - 1) * fdlp::kMaxChains * p->nlags) !=
+       hipMalloc((void**)&p->r_flat_part, sizeof(double) * (F * (p->sk.fl_H - 1) * fdlp::kMaxChains * p->nlags + fdlp::kRowSlack)) !=
            hipSuccess) ||
       hipMalloc((void**)&p->d_frames, sizeof(fdlp::FrameDesc) * F) != hipSuccess ||
       hipMalloc((void**)&p->d_utts, sizeof(fdlp::UttDesc) * F) != hipSuccess ||
