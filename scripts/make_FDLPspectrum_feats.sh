@@ -7,7 +7,8 @@
 # HIP -- HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES if set, else the KFD
 # topology's GPU nodes -- so a recipe that calls the driver unchanged, e.g. --cmd "$train_cmd" --nj 20
 # (e2e/wsj/run_fdlp_e1.sh:196), spreads its JOBs over the node), --jobs_per_gpu K (without $cmd: at most
-# N*K JOBs run at once; default 4), --job_mem / --job_gpu (the resource request a $cmd launcher gets for
+# N*K JOBs run at once; default 4), --chain_jobs (without $cmd, default true: those N*K slots are warm
+# processes running their JOBs in turn, featgen/job_chain.py), --job_mem / --job_gpu (the resource request a $cmd launcher gets for
 # every JOB: "$cmd --mem 5G --gpu 1 JOB=1:$nj ...", the reference's --mem 5G (:92, :141) plus one GPU, so
 # queue.pl / slurm.pl allocate the MI355X the JOB runs on; run.pl ignores both; --job_gpu 0 drops it),
 # --resume true (per-JOB resume: every JOB that finishes leaves <feat_dir>/melspec_<name>.JOB.done holding
@@ -51,6 +52,9 @@ noise_seed=
 job_mem=5G     # $cmd --mem (the reference driver's request, make_FDLPspectrum_feats.sh:92, :141)
 job_gpu=1      # $cmd --gpu (0: no GPU request)
 resume=false   # skip JOBs whose last finished run had the same shard and options (and whose outputs exist)
+chain_jobs=true  # without $cmd: the N*K concurrent slots are warm processes that run their JOBs one after the
+                 # other (featgen/job_chain.py: each JOB's own shard, outputs and log), so only a slot's first
+                 # JOB pays the cold start; false: one cold process per JOB, as the reference driver
 
 if [ -f utils/parse_options.sh ]; then
   . utils/parse_options.sh || exit 1
@@ -182,6 +186,28 @@ run_jobs() {  # run_jobs <list-pattern containing JOB> <scp-type-opt>
     return 0
   fi
   local pids=() jobs=() fail=0
+  if $chain_jobs; then
+    # slots per GPU: JOB n runs on GPU (n-1) mod ngpu (--device_rr), so each chain holds JOBs of one GPU
+    local d s k nslot=() chains=()
+    for n in "${pending[@]}"; do
+      d=$(( (n - 1) % ngpu ))
+      k=${nslot[$d]:-0}
+      s=$(( d * jobs_per_gpu + k % jobs_per_gpu ))
+      chains[$s]="${chains[$s]:+${chains[$s]},}$n"
+      nslot[$d]=$(( k + 1 ))
+    done
+    for s in "${!chains[@]}"; do
+      python3 "$here/speech_recognition_tools_amd/featgen/job_chain.py" --jobs "${chains[$s]}" \
+        --log "$log_dir/feats_${name}.JOB.log" --key "$log_dir/resume_${name}.JOB.key" \
+        --done "$feat_dir/melspec_${name}.JOB.done" --cli "$cli" -- \
+        "$pattern" "$feat_dir/melspec_${name}.JOB" $add_opts $cmvn_opt $stype --device_rr=JOB,$ngpu $feat_opts \
+        > "$log_dir/chain_${name}.$s.log" 2>&1 &
+      pids+=($!)
+    done
+    for s in "${!pids[@]}"; do wait "${pids[$s]}" || fail=1; done
+    [ $fail -eq 0 ] || { echo "$0: a JOB failed, see $log_dir/feats_${name}.*.log"; exit 1; }
+    return 0
+  fi
   for n in "${pending[@]}"; do
     python3 "$cli" "${pattern//JOB/$n}" "$feat_dir/melspec_${name}.$n" $add_opts ${cmvn_opt//JOB/$n} $stype \
       --device_rr=$n,$ngpu $feat_opts > "$log_dir/feats_${name}.$n.log" 2>&1 &

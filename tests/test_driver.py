@@ -318,3 +318,58 @@ def test_cli_unknown_option_exits_2_cleanly(tmp_path):
     r = subprocess.run(["bash", cli, "a.scp", str(tmp_path / "o"), "--no_such_option"],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 2 and "unrecognized arguments" in r.stderr
+
+
+CHAIN_CLI = r'''
+import os, sys
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+lst, out = args[0], args[1]
+print("job", out, "pid", os.getpid(), "keep_warm", "--keep_warm" in sys.argv)
+with open(os.environ["FAKE_CLI_LOG"], "a") as f:
+    f.write("%s %d\n" % (out, os.getpid()))
+if out.endswith(".4") and os.environ.get("FAIL_JOB4"):
+    raise RuntimeError("JOB 4 fails")
+utts = [l.split()[0] for l in open(lst) if l.strip()]
+open(out + ".ark", "w").write("ark")
+open(out + ".scp", "w").write("".join("%s %s.ark:%d\n" % (u, out, i) for i, u in enumerate(utts)))
+open(out + ".len", "w").write("".join("%s 1\n" % u for u in utts))
+'''
+
+
+@pytest.mark.parametrize("fail", [False, True])
+def test_driver_chains_run_jobs_in_warm_processes(tmp_path, fail):
+    """Without $cmd the driver's N*K slots are JOB chains (featgen/job_chain.py): 7 JOBs on 2 GPUs at 2 per
+    GPU run in 4 processes, each chain's JOBs on one GPU, every JOB with its own log, outputs and done
+    stamp and with --keep_warm; a failing JOB fails the driver but not the rest of its chain."""
+    src = tmp_path / "src" / "featgen"
+    src.mkdir(parents=True)
+    (src / "computeFDLPSpectrogram.py").write_text(CHAIN_CLI)
+    data = tmp_path / "data" / "dev"
+    data.mkdir(parents=True)
+    (data / "wav.scp").write_text("".join("u%d /x/u%d.wav\n" % (i, i) for i in range(14)))
+    log = tmp_path / "cli.log"
+    env = dict(os.environ, FAKE_CLI_LOG=str(log))
+    if fail:
+        env["FAIL_JOB4"] = "1"
+    cmd = ["bash", os.path.join(ROOT, "scripts", "make_FDLPspectrum_feats.sh"), "--nj", "7", "--ngpu", "2",
+           "--jobs_per_gpu", "2", "--src_dir", str(tmp_path / "src"), "--write_utt2num_frames", "true",
+           str(data), str(tmp_path / "fbank")]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=120)
+    ran = [l.split() for l in log.read_text().splitlines()]
+    assert sorted(int(o.rsplit(".", 1)[1]) for o, _ in ran) == list(range(1, 8))
+    pids = {}
+    for o, pid in ran:
+        pids.setdefault(pid, []).append(int(o.rsplit(".", 1)[1]))
+    assert len(pids) == 4
+    for jobs in pids.values():  # one GPU per chain: JOB n on GPU (n - 1) mod 2
+        assert len({(n - 1) % 2 for n in jobs}) == 1
+    for n in range(1, 8):
+        text = (data / "log" / ("feats_dev.%d.log" % n)).read_text()
+        assert ("melspec_dev.%d " % n) in text and "keep_warm True" in text
+        assert (tmp_path / "fbank" / ("melspec_dev.%d.done" % n)).exists() == (not (fail and n == 4))
+    if fail:
+        assert r.returncode != 0
+        assert "JOB 4 fails" in (data / "log" / "feats_dev.4.log").read_text()
+    else:
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert len((data / "feats.scp").read_text().splitlines()) == 14
