@@ -10,7 +10,7 @@ for the runtime's hipMemcpyAsync and for a copy kernel (benchmarks/d2h_copy.hip:
 host buffer through its device mapping, 16 bytes per lane) with W workgroups.  One JSON line per case.
 
     hipcc -O3 --offload-arch=gfx950 -shared -fPIC benchmarks/d2h_copy.hip -o benchmarks/libd2h_copy.so
-    GPU_MAX_HW_QUEUES=8 python benchmarks/d2h_probe.py
+    GPU_MAX_HW_QUEUES=8 python benchmarks/d2h_probe.py [--pipeline [--k=K] VARIANT...]
 """
 import ctypes
 import json
@@ -38,7 +38,7 @@ def main():
     dev = torch.device("cuda", 0)
     pcm_h = torch.from_numpy(utterance_pcm(full)).pin_memory()
     pcm = pcm_h.to(dev)
-    K = 4
+    K = int(next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--k=")), 4))  # batches in flight
     plans = [FdlpPlan(cfg, device=0, max_frames=frames) for _ in range(K)]
     outs = [torch.empty((rows, cfg.nfilters), dtype=torch.float32, device=dev) for _ in range(K)]
     streams = [torch.cuda.Stream(dev) for _ in range(K)]
