@@ -134,6 +134,7 @@ def pipeline(torch, dev, plans, streams, pcm_h, lens, nj, rng, rows, cfg, kern, 
     s_out = [torch.cuda.Stream(dev) for _ in range(8)]
     audio_h = sum(lens) / 16000.0 / 3600.0
     variants = [v for v in sys.argv[1:] if not v.startswith("-")] or ["stream", "compute", "kernel64"]
+    same_stream = "--same-stream" in sys.argv  # every batch's kernels on one compute stream (serialised)
     for variant in variants + variants:
         ev_done = [torch.cuda.Event() for _ in range(NB)]
         ev_out = [torch.cuda.Event() for _ in range(NB)]
@@ -154,7 +155,7 @@ def pipeline(torch, dev, plans, streams, pcm_h, lens, nj, rng, rows, cfg, kern, 
             it[0] += 1
             for b in range(K):
                 i = 2 * b + par
-                cs = streams[b]
+                cs = streams[0 if same_stream else b]
                 s_in.wait_event(ev_done[i])
                 with torch.cuda.stream(s_in):
                     if h2d_wgs:

@@ -5,8 +5,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-d2hk}; mkdir -p $O; : > $O/d2h_k.jsonl
-for k in 1 2 4; do
-  echo "# --k=$k" >> $O/d2h_k.jsonl
-  timeout -k 10 300 python3 benchmarks/d2h_probe.py --pipeline --k=$k stream >> $O/d2h_k.jsonl 2> $O/err.log || { tail -20 $O/err.log; exit 1; }
+for k in ${KS:-1 2 4}; do
+  echo "# --k=$k ${EXTRA:-}" >> $O/d2h_k.jsonl
+  timeout -k 10 300 python3 benchmarks/d2h_probe.py --pipeline --k=$k ${EXTRA:-} ${VARIANTS:-stream} >> $O/d2h_k.jsonl 2> $O/err.log || { tail -20 $O/err.log; exit 1; }
 done
 cat $O/d2h_k.jsonl
