@@ -49,6 +49,14 @@ def _parse(argv):
     return jobs, opts["--log"], opts["--key"], opts["--done"], opts["--cli"], cli
 
 
+def _libc_flush():
+    try:
+        import ctypes
+        ctypes.CDLL(None).fflush(None)
+    except (OSError, AttributeError):
+        pass
+
+
 def _sub(s, n):
     return s.replace("JOB", str(n))
 
@@ -83,6 +91,7 @@ def main(argv=None):
                     traceback.print_exc()
                 sys.stdout.flush()
                 sys.stderr.flush()
+                _libc_flush()  # the native runner's progress lines (C stdio) belong to this JOB's log
                 os.dup2(saved[0], 1)
                 os.dup2(saved[1], 2)
             if ok and key_pat and done_pat:
