@@ -285,19 +285,16 @@ def _run_native(args, cfg, device, noise, snr, diff):
     return None
 
 
-_RELEASE_REGISTERED = False
-
-
 def _register_job_release():
     """--keep_warm parks the plan, streams and pinned slots in the library; include/fdlp.h asks for
     fdlp_job_release before the HIP runtime is torn down, so the process releases them at exit."""
-    global _RELEASE_REGISTERED
-    if _RELEASE_REGISTERED:
-        return
     import atexit
     from speech_recognition_tools_amd import _lib
+    # the flag lives in the library module: a JOB chain (featgen/job_chain.py) re-runs this file per JOB
+    if getattr(_lib, "_job_release_registered", False):
+        return
     atexit.register(_lib.lib.fdlp_job_release)
-    _RELEASE_REGISTERED = True
+    _lib._job_release_registered = True
 
 
 LAST_JOB_STATS = None  # fdlp_job_stats of the last native run (benchmarks/cli_throughput.py reports it)
