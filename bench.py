@@ -507,8 +507,19 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
     widen_pool = ThreadPoolExecutor(1)               # one widening job at a time, each on 16 threads
     widen_jobs = [None] * NB
     widen_s = [0.0]
+    host_issue = args.xfer_d2h_issue == "host"
+    issue_pool = ThreadPoolExecutor(1) if host_issue else None
+    issue_jobs = [None] * NB
+
+    def issue_d2h(i, so):                            # --xfer-d2h-issue host: no device-side wait before the copy
+        ev_done[i].synchronize()
+        with torch.cuda.stream(so):
+            q_h[i].copy_(q_d[i], non_blocking=True)
+            ev_out[i].record(so)
 
     def widen(i):
+        if issue_jobs[i] is not None:
+            issue_jobs[i].result()                   # ev_out[i] is recorded
         ev_out[i].synchronize()                      # the codes of buffer set i are on the host
         t0 = time.perf_counter()
         q_widen(q_h[i][:nq], 3, threads=16, out=f_h[i])
@@ -531,10 +542,13 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
                              q_flag=flag, **mix[b])
             ev_done[i].record(cs)
         so = s_outs[b % nd]
-        so.wait_event(ev_done[i])
-        with torch.cuda.stream(so):
-            q_h[i].copy_(q_d[i], non_blocking=True)
-            ev_out[i].record(so)
+        if host_issue:
+            issue_jobs[i] = issue_pool.submit(issue_d2h, i, so)
+        else:
+            so.wait_event(ev_done[i])
+            with torch.cuda.stream(so):
+                q_h[i].copy_(q_d[i], non_blocking=True)
+                ev_out[i].record(so)
         widen_jobs[i] = widen_pool.submit(widen, i)
 
     def xstep():
@@ -558,6 +572,8 @@ def pcie_pass(args, plans, streams, pcms, outs, pcm_host, lens, nj, rng, mix, au
         t_go[0] = time.time()  # absolute start of the timed region (the ranks' children combine on the union)
     el_x = timed_steps(xstep, args.steps, args.warmup, xsync, dd, cpu_dev, before_timed=mark_start)
     widen_pool.shutdown()
+    if issue_pool is not None:
+        issue_pool.shutdown()
     flags = [int(q[nq:].view(torch.int32)[0]) for q in q_h]
     # the last step's widened codes equal the float32 rows still in HBM (bit-identical)
     par = (it[0] - 1) % S
@@ -595,6 +611,11 @@ def parse_args(argv=None):
     ap.add_argument("--xfer-d2h-streams", type=int, default=0,
                     help="PCIe pass: device-to-host copy streams (0: two in the child process that has its own "
                          "hardware queues, one in-process, where more streams share queues with the kernels)")
+    ap.add_argument("--xfer-d2h-issue", choices=["stream", "host"], default="host",
+                    help="PCIe pass: a batch's D2H copy is issued by a host thread once the batch's event has "
+                         "completed (host, the default: no device-side wait) or waits for its kernels on the D2H "
+                         "stream (stream: the copy's span falls into a 5.14 ms quantum as soon as two batches are in "
+                         "flight, profiles/r06l_d2h_inflight.jsonl; ratio 0.79-0.85 against 0.91-0.93, r06s)")
     ap.add_argument("--xfer-hw-queues", type=int, default=8,
                     help="PCIe pass: every rank runs it in a child process (started before the rank touches the "
                          "GPU) with GPU_MAX_HW_QUEUES set to this (the compute, H2D and D2H streams then get hardware "
