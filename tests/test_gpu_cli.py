@@ -347,6 +347,49 @@ def test_driver_script_two_jobs(tmp_path):
     assert np.max(np.abs(got - want) / np.maximum(np.abs(want), 1.0)) <= 1e-12
 
 
+def test_driver_chained_jobs_write_cold_jobs_bytes(tmp_path):
+    """The driver's warm JOB chains (--chain_jobs true: 5 JOBs in 2 processes, a plan and slots reused and
+    the jitter generator re-seeded per JOB) write every JOB's .ark / .len and the data dir's feats.scp /
+    utt2num_frames byte for byte as one cold process per JOB does (--chain_jobs false).  --seed is given:
+    unseeded, the OLA jitter draws from OS entropy per JOB, as the reference's random module does, and
+    two runs of either mode differ (benchmarks/job_determinism.py, profiles/r06x_job_determinism.jsonl)."""
+    import subprocess
+    from conftest import ROOT
+    meta, _, _, _ = load_golden("wsj")
+    rng = np.random.default_rng(23)
+    utts = ["c%03d" % i for i in range(25)]
+    sig = {u: np.clip(rng.standard_normal(int(rng.integers(16000, 64000))) * 2500, -32768, 32767).astype(np.int16)
+           for u in utts}
+    o = meta["opts"]
+    got = {}
+    for chain in ("true", "false"):
+        data = tmp_path / chain / "data"
+        data.mkdir(parents=True)
+        _write_scp(str(data), sig, utts)
+        fb = tmp_path / chain / "fbank"
+        cmd = ["bash", os.path.join(ROOT, "scripts", "make_FDLPspectrum_feats.sh"), "--nj", "5", "--ngpu", "1",
+               "--jobs_per_gpu", "2", "--chain_jobs", chain, "--seed", "7", "--nfilters", str(o["nfilters"]),
+               "--order", str(o["order"]), "--fduration", str(o["fduration"]), "--frate", str(o["frate"]),
+               "--coeff_range", o["coeff_range"], "--coeff_num", str(o["coeff_num"]),
+               "--overlap_fraction", str(o["overlap_fraction"]), "--fbank_type", o["fbank_type"],
+               "--write_utt2num_frames", "true", str(data), str(fb)]
+        r = subprocess.run(cmd, cwd=str(tmp_path / chain), capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stdout + r.stderr
+        files = {}
+        for n in range(1, 6):
+            for ext in (".ark", ".len"):
+                p = fb / ("melspec_data.%d%s" % (n, ext))
+                files[p.name] = p.read_bytes()
+        feats = [l.split() for l in open(str(data / "feats.scp"))]
+        files["feats.scp"] = [(k, v.rsplit("/", 1)[1]) for k, v in feats]  # paths differ by the run dir
+        files["utt2num_frames"] = (data / "utt2num_frames").read_text()
+        got[chain] = files
+    assert [k for k, _ in got["true"]["feats.scp"]] == utts
+    assert got["true"].keys() == got["false"].keys()
+    for k in got["true"]:
+        assert got["true"][k] == got["false"][k], k
+
+
 @pytest.mark.parametrize("name", ["reverb_rir", "reverb_rir_noise"])
 def test_cli_add_reverb(tmp_path, monkeypatch, name):
     """--add_reverb small_room reads ./RIR/RIR_SmallRoom1_near_AnglA.wav (channel 1 / 2^15) and
