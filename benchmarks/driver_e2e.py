@@ -181,7 +181,8 @@ def main():
         single = _check_single(a, base, data) if a.check_single else None
         from speech_recognition_tools_amd.shard import visible_gpu_count
         ngpu = a.ngpu or max(1, visible_gpu_count())  # the driver's own rule
-        print(json.dumps({"metric": "recipe stage-1 end-to-end audio-hours/s (make_FDLPspectrum_feats.sh, cold JOBs)",
+        print(json.dumps({"metric": "recipe stage-1 end-to-end audio-hours/s (make_FDLPspectrum_feats.sh, %s)"
+                          % ("warm JOB chains" if a.chain_jobs == "true" else "a cold process per JOB"),
                           "value": audio_h / wall, "unit": "audio-hours/s", "wall_s": wall, "audio_hours": audio_h,
                           "utts": a.utts, "utt_seconds": "U(%g,%g)" % tuple(a.lengths), "nj": a.nj,
                           "jobs_per_gpu": a.jobs_per_gpu, "chain_jobs": a.chain_jobs == "true", "ngpu": ngpu,
